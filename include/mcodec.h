@@ -1,0 +1,192 @@
+/*
+ * mcodec.h -- C ABI of libmcodec.so, the MI355X (gfx950) kernels behind
+ * numcodecs_amd.
+ *
+ * This is the drop-in boundary for numcodecs' per-element filter codecs and
+ * its Fletcher32 checksum.  Every entry point takes plain device pointers,
+ * byte/element counts and a hipStream_t (passed as `mc_stream_t`, NULL = the
+ * legacy default stream).  Entry points never allocate device memory, never
+ * synchronise the stream and never throw: they enqueue kernels and return a
+ * status (MC_OK, a negative MC_E* code, or MC_EHIP_BASE - hipError_t).
+ * Argument checks that numcodecs reports as Python exceptions are done by the
+ * host layer (the numcodecs_amd Python modules) before the call; the library re-checks what
+ * it needs for memory safety and returns MC_EINVAL.
+ *
+ * Reference interface each entry point replaces (paths relative to the
+ * numcodecs source tree, src/numcodecs/):
+ *   mc_shuffle / mc_unshuffle ...... _shuffle.pyx:11-18 _doShuffle / :23-30 _doUnshuffle
+ *                                    (called from shuffle.py:40-58 Shuffle.encode/decode)
+ *   mc_bitround .................... bitround.py:45-69 BitRound.encode (numpy int ops)
+ *   mc_bitround_shuffle ............ bitround.py:45-69 followed by _shuffle.pyx:11-18, fused
+ *   mc_delta_encode ................ delta.py:52-67 Delta.encode (np.diff)
+ *   mc_delta_decode ................ delta.py:69-83 Delta.decode (np.cumsum)
+ *   mc_fso_encode / mc_fso_decode .. fixedscaleoffset.py:83-97 / :99-113
+ *   mc_quantize .................... quantize.py:60-76 Quantize.encode
+ *   mc_cast ........................ ndarray.astype as used by quantize.py:76,80,
+ *                                    fixedscaleoffset.py:97,110, compat.py:177-206
+ *   mc_fletcher32* ................. fletcher32.pyx:24-57 _fletcher32, :75-89 encode,
+ *                                    :91-115 decode; _utils.pxd:11-24 store/load_le32
+ *   *_batch ........................ no reference counterpart: the Zarr caller loops
+ *                                    Codec.encode per chunk; these run B equal-size
+ *                                    chunks in one launch (chunk b at base + b*stride).
+ */
+#ifndef MCODEC_H
+#define MCODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *mc_stream_t; /* hipStream_t */
+
+#define MC_ABI_VERSION 1
+
+/* status codes */
+#define MC_OK 0
+#define MC_EINVAL (-22)      /* bad argument (size, dtype, alignment, NULL) */
+#define MC_ENOSPC (-28)      /* workspace too small */
+#define MC_EHIP_BASE (-1000) /* MC_EHIP_BASE - (int)hipError_t */
+
+/* dtype codes (little-endian numpy dtypes; numpy kind + itemsize) */
+enum mc_dtype {
+  MC_B1 = 0, /* '|b1' bool */
+  MC_I1 = 1, /* '|i1' */
+  MC_I2 = 2, /* '<i2' */
+  MC_I4 = 3, /* '<i4' */
+  MC_I8 = 4, /* '<i8' */
+  MC_U1 = 5, /* '|u1' */
+  MC_U2 = 6, /* '<u2' */
+  MC_U4 = 7, /* '<u4' */
+  MC_U8 = 8, /* '<u8' */
+  MC_F2 = 9, /* '<f2' */
+  MC_F4 = 10, /* '<f4' */
+  MC_F8 = 11, /* '<f8' */
+  MC_NDTYPES = 12
+};
+
+int mc_abi_version(void);
+const char *mc_strerror(int status);
+/* number of HIP devices visible to the runtime the library is bound to */
+int mc_device_count(void);
+
+/* ---- Shuffle ---------------------------------------------------------- */
+/* Byte transpose of the (nbytes/elementsize, elementsize) byte matrix:
+ *   dst[b*count + i] = src[i*elementsize + b],  count = nbytes/elementsize.
+ * nbytes % elementsize must be 0; elementsize >= 1 (1 is a plain copy).
+ * src and dst must not overlap. */
+int mc_shuffle(const void *src, void *dst, size_t nbytes, size_t elementsize,
+               mc_stream_t stream);
+/* Inverse: dst[i*elementsize + b] = src[b*count + i]. */
+int mc_unshuffle(const void *src, void *dst, size_t nbytes, size_t elementsize,
+                 mc_stream_t stream);
+/* Batched: nchunks independent chunks of chunk_bytes each; chunk c is read at
+ * src + c*src_stride and written at dst + c*dst_stride (strides in bytes). */
+int mc_shuffle_batch(const void *src, size_t src_stride, void *dst,
+                     size_t dst_stride, size_t nchunks, size_t chunk_bytes,
+                     size_t elementsize, mc_stream_t stream);
+int mc_unshuffle_batch(const void *src, size_t src_stride, void *dst,
+                       size_t dst_stride, size_t nchunks, size_t chunk_bytes,
+                       size_t elementsize, mc_stream_t stream);
+
+/* ---- BitRound --------------------------------------------------------- */
+/* n elements of itemsize 2 (f16), 4 (f32) or 8 (f64); 0 <= keepbits < max
+ * mantissa bits (10/23/52).  dst receives the rounded bit patterns. */
+int mc_bitround(const void *src, void *dst, size_t n, int itemsize,
+                int keepbits, mc_stream_t stream);
+/* BitRound then Shuffle(elementsize=itemsize) in one pass (dst = shuffled). */
+int mc_bitround_shuffle(const void *src, void *dst, size_t n, int itemsize,
+                        int keepbits, mc_stream_t stream);
+
+/* ---- Delta ------------------------------------------------------------ */
+/* dst[0] = astype(src[0]); dst[i] = astype(src[i] - src[i-1]) computed in
+ * dtype (bool: src[i] != src[i-1]).  n >= 1. */
+int mc_delta_encode(const void *src, void *dst, size_t n, int dtype,
+                    int astype, mc_stream_t stream);
+/* dst = cumsum(dtype(src)) accumulated in dtype (bool: logical or).  Integer
+ * dtypes use a parallel scan (modular arithmetic, bit-exact); float dtypes
+ * keep numpy's sequential left-to-right rounding (serial per chunk). */
+size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
+int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
+                    int dtype, void *workspace, size_t workspace_bytes,
+                    mc_stream_t stream);
+
+/* ---- FixedScaleOffset / Quantize / casts ------------------------------ */
+/* Scalars arrive already converted (on the host, by numpy's NEP 50 rules) to
+ * the compute dtype of the operation that uses them: *_f for float compute
+ * dtypes, *_i for integer compute dtypes.
+ * encode: dst = astype(rint((dtype(x) -[t1] offset) *[t2] scale)) */
+int mc_fso_encode(const void *src, void *dst, size_t n, int dtype, int t1,
+                  int t2, int astype, double offset_f, int64_t offset_i,
+                  double scale_f, int64_t scale_i, mc_stream_t stream);
+/* decode: dst = dtype((astype(x) /[t3] scale) +[t4] offset); t3, t4 float */
+int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3,
+                  int t4, int dtype, double scale, double offset,
+                  mc_stream_t stream);
+/* Quantize encode: dst = astype(rint(scale *[dtype] x) /[dtype] scale) */
+int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype,
+                double scale, mc_stream_t stream);
+/* numpy `astype` (unsafe casting; x86-64 results for out-of-range/NaN
+ * float->int, correctly rounded float narrowing). */
+int mc_cast(const void *src, void *dst, size_t n, int from_dtype,
+            int to_dtype, mc_stream_t stream);
+
+/* ---- Fletcher32 ------------------------------------------------------- */
+size_t mc_fletcher32_workspace(size_t nbytes);
+/* *out_sum (device) = fletcher32(src[0:nbytes]); nbytes >= 0. */
+int mc_fletcher32(const void *src, size_t nbytes, uint32_t *out_sum,
+                  void *workspace, size_t workspace_bytes, mc_stream_t stream);
+/* dst[0:nbytes] = src; dst[nbytes:nbytes+4] = LE32(fletcher32(src)). */
+int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes,
+                         void *workspace, size_t workspace_bytes,
+                         mc_stream_t stream);
+/* out_pair (device, 2 words) = {fletcher32(src[0:nbytes-4]),
+ * LE32(src[nbytes-4:nbytes])}; nbytes >= 4. */
+int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair,
+                         void *workspace, size_t workspace_bytes,
+                         mc_stream_t stream);
+/* out_sums[c] = fletcher32(chunk c), chunk c = src + c*stride, chunk_bytes. */
+size_t mc_fletcher32_batch_workspace(size_t nchunks, size_t chunk_bytes);
+int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks,
+                        size_t chunk_bytes, uint32_t *out_sums,
+                        void *workspace, size_t workspace_bytes,
+                        mc_stream_t stream);
+
+/* ---- fused chunk pipelines (Zarr filter chain -> checksum) ------------- */
+/* Workspace for the two calls below. */
+size_t mc_shuffle_fletcher32_workspace(size_t nchunks, size_t chunk_bytes,
+                                       size_t elementsize);
+/* Per chunk: enc = Shuffle(es).encode(chunk) ++ LE32(fletcher32(enc)).
+ * dst chunk c at dst + c*dst_stride, dst_stride >= chunk_bytes + 4 (a
+ * multiple of 16 keeps the single-pass fused kernel). */
+int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride,
+                                       void *dst, size_t dst_stride,
+                                       size_t nchunks, size_t chunk_bytes,
+                                       size_t elementsize, void *workspace,
+                                       size_t workspace_bytes,
+                                       mc_stream_t stream);
+/* Per chunk: verify the footer of src chunk (chunk_bytes + 4 bytes) and
+ * unshuffle the payload into dst.  status[2c] = computed checksum,
+ * status[2c+1] = stored footer (device array of 2*nchunks words). */
+int mc_fletcher32_unshuffle_batch(const void *src, size_t src_stride,
+                                  void *dst, size_t dst_stride,
+                                  size_t nchunks, size_t chunk_bytes,
+                                  size_t elementsize, uint32_t *status,
+                                  void *workspace, size_t workspace_bytes,
+                                  mc_stream_t stream);
+
+/* ---- tuning / measurement hooks (bench.py) ----------------------------- */
+/* Shuffle with an explicit kernel variant and grid (0 = default); used by
+ * bench.py to sweep variants.  variant: 0 default, 1 register/dword stores,
+ * 2 LDS-staged 16-B stores, 3 LDS both sides, 4 generic byte kernel. */
+int mc_shuffle_variant(const void *src, void *dst, size_t nbytes,
+                       size_t elementsize, int encode, int variant,
+                       int max_blocks, mc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCODEC_H */

@@ -1,0 +1,74 @@
+"""numcodecs_amd -- numcodecs' per-element filter codecs and Fletcher32 on AMD
+Instinct MI355X (gfx950).
+
+A drop-in for the hot path of zarr-developers/numcodecs: the codecs
+Shuffle, BitRound, Delta, Quantize, FixedScaleOffset and Fletcher32 with the
+same ids, configs, reprs and error behaviour, executed by hand-written HIP
+kernels (libmcodec.so, C ABI in include/mcodec.h) on device-resident chunks.
+Device tensors stay on the device; host buffers are staged through it.
+
+Reference registrations: src/numcodecs/__init__.py:74,78,82,102,106,127.
+"""
+
+from .abc import Codec
+from .errors import UnknownCodecError
+from .registry import codec_registry, get_codec, register_codec
+
+from .delta import Delta
+
+register_codec(Delta)
+
+from .quantize import Quantize
+
+register_codec(Quantize)
+
+from .fixedscaleoffset import FixedScaleOffset
+
+register_codec(FixedScaleOffset)
+
+from .shuffle import Shuffle
+
+register_codec(Shuffle)
+
+from .bitround import BitRound
+
+register_codec(BitRound)
+
+from .fletcher32 import Fletcher32
+
+register_codec(Fletcher32)
+
+from . import batch  # noqa: E402,F401  (batched chunk API and fused pipelines)
+
+__version__ = "0.1.0"
+
+__all__ = [
+    "BitRound",
+    "Codec",
+    "Delta",
+    "FixedScaleOffset",
+    "Fletcher32",
+    "Quantize",
+    "Shuffle",
+    "UnknownCodecError",
+    "batch",
+    "codec_registry",
+    "get_codec",
+    "register_codec",
+]
+
+
+def register_with_numcodecs():
+    """Register these classes into an installed ``numcodecs`` registry
+    (replacing the CPU implementations under the same ids).  Returns the
+    list of ids registered, or [] when numcodecs is not importable."""
+    try:
+        import numcodecs  # noqa: F401
+        from numcodecs.registry import register_codec as _nc_register
+    except Exception:
+        return []
+    ids = []
+    for cls in (Delta, Quantize, FixedScaleOffset, Shuffle, BitRound, Fletcher32):
+        _nc_register(cls)
+        ids.append(cls.codec_id)
+    return ids

@@ -1,0 +1,186 @@
+"""ctypes binding of libmcodec.so (the C ABI declared in include/mcodec.h).
+
+The library is a plain C-ABI shared object built by hipcc for gfx950
+(numcodecs_amd/csrc/Makefile).  It is bound to the HIP runtime that torch has
+already loaded: torch is imported first, so the library's NEEDED
+``libamdhip64.so.7`` resolves (by soname) to torch's copy and both share one
+runtime, one device context and torch's streams.
+
+There is no CPU fallback anywhere in the product path: if the library is
+missing, or no HIP device is visible, every codec call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- must precede the dlopen below (shared HIP runtime)
+
+__all__ = [
+    "DTYPE_CODES",
+    "MCodecError",
+    "lib",
+    "lib_path",
+    "check",
+    "available",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.environ.get("NUMCODECS_AMD_LIB", os.path.join(_HERE, "_lib", "libmcodec.so"))
+
+# mc_dtype codes (include/mcodec.h)
+DTYPE_CODES = {
+    "|b1": 0,
+    "|i1": 1,
+    "<i2": 2,
+    "<i4": 3,
+    "<i8": 4,
+    "|u1": 5,
+    "<u2": 6,
+    "<u4": 7,
+    "<u8": 8,
+    "<f2": 9,
+    "<f4": 10,
+    "<f8": 11,
+}
+
+MC_OK = 0
+MC_EINVAL = -22
+MC_ENOSPC = -28
+MC_EHIP_BASE = -1000
+
+
+class MCodecError(RuntimeError):
+    """A libmcodec entry point returned a non-zero status."""
+
+
+_c_size = ctypes.c_size_t
+_c_int = ctypes.c_int
+_c_vp = ctypes.c_void_p
+_c_double = ctypes.c_double
+_c_i64 = ctypes.c_int64
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGNATURES = {
+    "mc_abi_version": [],
+    "mc_strerror": [_c_int],
+    "mc_device_count": [],
+    "mc_shuffle": [_c_vp, _c_vp, _c_size, _c_size, _c_vp],
+    "mc_unshuffle": [_c_vp, _c_vp, _c_size, _c_size, _c_vp],
+    "mc_shuffle_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp],
+    "mc_unshuffle_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp],
+    "mc_bitround": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
+    "mc_bitround_shuffle": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
+    "mc_delta_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
+    "mc_delta_decode_workspace": [_c_size, _c_int, _c_int],
+    "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
+    "mc_fso_encode": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int,
+        _c_double, _c_i64, _c_double, _c_i64, _c_vp,
+    ],
+    "mc_fso_decode": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int, _c_double, _c_double, _c_vp,
+    ],
+    "mc_quantize": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_vp],
+    "mc_cast": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
+    "mc_fletcher32_workspace": [_c_size],
+    "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_verify": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_batch_workspace": [_c_size, _c_size],
+    "mc_fletcher32_batch": [_c_vp, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
+    "mc_shuffle_fletcher32_workspace": [_c_size, _c_size, _c_size],
+    "mc_shuffle_fletcher32_encode_batch": [
+        _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_fletcher32_unshuffle_batch": [
+        _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_shuffle_variant": [_c_vp, _c_vp, _c_size, _c_size, _c_int, _c_int, _c_int, _c_vp],
+}
+_RESTYPES = {
+    "mc_strerror": ctypes.c_char_p,
+    "mc_delta_decode_workspace": ctypes.c_size_t,
+    "mc_fletcher32_workspace": ctypes.c_size_t,
+    "mc_fletcher32_batch_workspace": ctypes.c_size_t,
+    "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
+}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lock = threading.Lock()
+_lib = None
+_load_error: Exception | None = None
+
+
+def _load():
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(lib_path):
+            _load_error = MCodecError(
+                f"libmcodec.so not found at {lib_path}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C numcodecs_amd/csrc)"
+            )
+            raise _load_error
+        handle = ctypes.CDLL(lib_path)
+        missing = []
+        for name, argtypes in _SIGNATURES.items():
+            try:
+                fn = getattr(handle, name)
+            except AttributeError:
+                missing.append(name)
+                continue
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        if missing:
+            _load_error = MCodecError(f"libmcodec.so is missing symbols: {missing}")
+            raise _load_error
+        _lib = handle
+        return _lib
+
+
+class _LibProxy:
+    """Attribute access loads the library on first use (import stays cheap)."""
+
+    def __getattr__(self, name):
+        return getattr(_load(), name)
+
+
+lib = _LibProxy()
+
+
+def check(status: int, what: str = "mcodec") -> None:
+    """Raise MCodecError for a non-zero libmcodec status."""
+    if status != MC_OK:
+        msg = lib.mc_strerror(status)
+        msg = msg.decode() if msg else "unknown"
+        raise MCodecError(f"{what} failed with status {status}: {msg}")
+
+
+def available() -> bool:
+    """True when the library loads and a HIP device is visible to it."""
+    try:
+        _load()
+    except Exception:
+        return False
+    return torch.cuda.is_available()
+
+
+def require_device() -> None:
+    """Fail loudly when there is no HIP device: no CPU fallback exists."""
+    _load()
+    if not torch.cuda.is_available():
+        raise MCodecError(
+            "numcodecs_amd requires a HIP device (MI355X/gfx950); none is visible. "
+            "There is no CPU fallback in the product path."
+        )
+
+
+def stream_handle(device=None) -> int:
+    """hipStream_t of torch's current stream on `device` (as an int)."""
+    return torch.cuda.current_stream(device).cuda_stream

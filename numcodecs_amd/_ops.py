@@ -1,0 +1,183 @@
+"""Thin wrappers over the libmcodec entry points (include/mcodec.h).
+
+Each wrapper takes device tensors, calls the C ABI on torch's current stream
+for the tensor's device, and raises on a non-zero status.  Nothing here
+synchronises except where a result must be inspected on the host
+(Fletcher32 verification).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import DTYPE_CODES, check, lib
+
+__all__ = ["dtype_code", "stream", "workspace"]
+
+
+def dtype_code(dt) -> int:
+    """mc_dtype code of numpy dtype `dt` (little-endian numeric types only)."""
+    dt = np.dtype(dt)
+    try:
+        return DTYPE_CODES[dt.str]
+    except KeyError:
+        raise NotImplementedError(
+            f"dtype {dt.str!r} is not supported by the numcodecs_amd device kernels "
+            "(little-endian bool/int/uint/float only)"
+        ) from None
+
+
+def stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
+
+
+def _guard(t: torch.Tensor):
+    return torch.cuda.device(t.device)
+
+
+# ---------------------------------------------------------------------------
+def shuffle(src: torch.Tensor, dst: torch.Tensor, nbytes: int, es: int, encode: bool) -> None:
+    _native.require_device()
+    if nbytes == 0:
+        return
+    with _guard(src):
+        fn = lib.mc_shuffle if encode else lib.mc_unshuffle
+        check(fn(src.data_ptr(), dst.data_ptr(), nbytes, es, stream(src)),
+              "mc_shuffle" if encode else "mc_unshuffle")
+
+
+def shuffle_batch(src, src_stride, dst, dst_stride, nchunks, chunk_bytes, es, encode) -> None:
+    _native.require_device()
+    with _guard(src):
+        fn = lib.mc_shuffle_batch if encode else lib.mc_unshuffle_batch
+        check(fn(src.data_ptr(), src_stride, dst.data_ptr(), dst_stride, nchunks, chunk_bytes, es,
+                 stream(src)), "mc_(un)shuffle_batch")
+
+
+def bitround(src, dst, n, itemsize, keepbits) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_bitround(src.data_ptr(), dst.data_ptr(), n, itemsize, keepbits, stream(src)),
+              "mc_bitround")
+
+
+def bitround_shuffle(src, dst, n, itemsize, keepbits) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_bitround_shuffle(src.data_ptr(), dst.data_ptr(), n, itemsize, keepbits,
+                                      stream(src)), "mc_bitround_shuffle")
+
+
+def delta_encode(src, dst, n, dtype, astype) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_delta_encode(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype),
+                                  dtype_code(astype), stream(src)), "mc_delta_encode")
+
+
+def delta_decode(src, dst, n, astype, dtype) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        a, d = dtype_code(astype), dtype_code(dtype)
+        ws_n = lib.mc_delta_decode_workspace(n, a, d)
+        ws = workspace(ws_n, src)
+        check(lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d, ws.data_ptr(), ws.numel(),
+                                  stream(src)), "mc_delta_decode")
+
+
+def _scalar_args(value, dt):
+    """(double, int64) pair carrying `value` in compute dtype `dt`."""
+    dt = np.dtype(dt)
+    if dt.kind == "f":
+        return float(value), 0
+    if dt.kind == "b":
+        return 0.0, int(bool(value))
+    arr = np.asarray(value, dtype=dt)
+    if dt.kind == "u" and dt.itemsize == 8:
+        return 0.0, int(arr.view(np.int64))
+    return 0.0, int(arr)
+
+
+def fso_encode(src, dst, n, dtype, t1, t2, astype, offset_t1, scale_t2) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    of, oi = _scalar_args(offset_t1, t1)
+    sf, si = _scalar_args(scale_t2, t2)
+    with _guard(src):
+        check(lib.mc_fso_encode(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype), dtype_code(t1),
+                                dtype_code(t2), dtype_code(astype), of, oi, sf, si, stream(src)),
+              "mc_fso_encode")
+
+
+def fso_decode(src, dst, n, astype, t3, t4, dtype, scale_t3, offset_t4) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_fso_decode(src.data_ptr(), dst.data_ptr(), n, dtype_code(astype), dtype_code(t3),
+                                dtype_code(t4), dtype_code(dtype), float(scale_t3), float(offset_t4),
+                                stream(src)), "mc_fso_decode")
+
+
+def quantize(src, dst, n, dtype, astype, scale) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_quantize(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype), dtype_code(astype),
+                              float(scale), stream(src)), "mc_quantize")
+
+
+def cast(src, dst, n, from_dt, to_dt) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_cast(src.data_ptr(), dst.data_ptr(), n, dtype_code(from_dt), dtype_code(to_dt),
+                          stream(src)), "mc_cast")
+
+
+def fletcher32_encode(src, dst, nbytes) -> None:
+    _native.require_device()
+    with _guard(src):
+        ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
+        check(lib.mc_fletcher32_encode(src.data_ptr(), dst.data_ptr(), nbytes, ws.data_ptr(),
+                                       ws.numel(), stream(src)), "mc_fletcher32_encode")
+
+
+def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
+    """(computed, stored) for a buffer of payload + 4-byte footer (syncs)."""
+    _native.require_device()
+    with _guard(src):
+        ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
+        pair = torch.empty(2, dtype=torch.int32, device=src.device)
+        check(lib.mc_fletcher32_verify(src.data_ptr(), nbytes, pair.data_ptr(), ws.data_ptr(),
+                                       ws.numel(), stream(src)), "mc_fletcher32_verify")
+        v = pair.cpu().numpy().view(np.uint32)
+    return int(v[0]), int(v[1])
+
+
+def fletcher32(src, nbytes) -> int:
+    """Checksum of the first `nbytes` of a device tensor (syncs)."""
+    _native.require_device()
+    with _guard(src):
+        ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
+        out = torch.empty(1, dtype=torch.int32, device=src.device)
+        check(lib.mc_fletcher32(src.data_ptr(), nbytes, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                stream(src)), "mc_fletcher32")
+        return int(out.cpu().numpy().view(np.uint32)[0])

@@ -1,0 +1,270 @@
+"""Batched chunk API and fused filter pipelines.
+
+numcodecs is called by Zarr once per chunk (``codec.encode(chunk)``), which
+on a GPU is launch-bound for small chunks (a 1 MiB chunk moves in ~0.3 us at
+HBM rate, far less than a kernel launch).  This module adds what the
+reference has no counterpart for:
+
+* ``*_chunks`` functions over a ``[B, chunk_bytes]`` batch of equal-size
+  chunks in one launch (chunk b at row b; rows may be padded);
+* :class:`FilterPipeline`, a Zarr-style filter chain (+ optional checksum)
+  that recognises fusable sequences and runs them as single kernels:
+  ``BitRound -> Shuffle`` (one pass), ``Shuffle -> Fletcher32`` (one pass,
+  checksum of the shuffled bytes computed in registers while they are
+  stored), and decodes ``Fletcher32 -> Shuffle`` with the verification fused
+  into the unshuffle.  Any other chain runs codec by codec on the device.
+
+Results are identical to applying the reference codecs one after another.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native, _ops
+from ._native import check, lib
+from .bitround import BitRound, max_bits
+from .compat import ensure_contiguous_ndarray, is_device_tensor
+from .fletcher32 import Fletcher32, _mismatch
+from .shuffle import Shuffle
+
+__all__ = [
+    "FilterPipeline",
+    "fletcher32_chunks",
+    "shuffle_chunks",
+    "unshuffle_chunks",
+    "shuffle_fletcher32_encode_chunks",
+    "fletcher32_unshuffle_decode_chunks",
+    "encoded_stride",
+]
+
+
+def _as_rows(chunks: torch.Tensor) -> torch.Tensor:
+    """[B, ...] device tensor -> [B, row_bytes] uint8 view (rows contiguous)."""
+    if not is_device_tensor(chunks):
+        raise TypeError("batched chunk functions take a device tensor [B, ...]")
+    if chunks.dim() < 1:
+        raise ValueError("expected a batch dimension")
+    b = chunks.shape[0]
+    rows = chunks.reshape(b, -1)
+    if rows.stride(1) != 1:
+        raise ValueError("each chunk must be contiguous")
+    rows = rows.view(torch.uint8) if rows.element_size() != 1 or rows.dtype != torch.uint8 else rows
+    return rows
+
+
+def encoded_stride(chunk_bytes: int) -> int:
+    """Row stride of an encoded batch: payload + 4-byte footer, padded to 256 B
+    so that every row stays 16-B aligned for the fused kernels."""
+    return (chunk_bytes + 4 + 255) // 256 * 256
+
+
+def shuffle_chunks(chunks, elementsize, out=None):
+    """Shuffle(elementsize).encode of every chunk of a [B, ...] device batch."""
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    out = torch.empty((b, n), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if b and n:
+        _ops.shuffle_batch(rows, rows.stride(0), out, out.stride(0), b, n, elementsize, True)
+    return out
+
+
+def unshuffle_chunks(chunks, elementsize, out=None):
+    """Shuffle(elementsize).decode of every chunk of a [B, ...] device batch."""
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    out = torch.empty((b, n), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if b and n:
+        _ops.shuffle_batch(rows, rows.stride(0), out, out.stride(0), b, n, elementsize, False)
+    return out
+
+
+def fletcher32_chunks(chunks, nbytes=None) -> torch.Tensor:
+    """Fletcher32 of every chunk (first `nbytes` of each row); int64 [B]."""
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    nbytes = n if nbytes is None else nbytes
+    res = torch.empty(b, dtype=torch.int32, device=rows.device)
+    if b:
+        _native.require_device()
+        with torch.cuda.device(rows.device):
+            ws = _ops.workspace(lib.mc_fletcher32_batch_workspace(b, nbytes), rows)
+            check(lib.mc_fletcher32_batch(rows.data_ptr(), rows.stride(0), b, nbytes, res.data_ptr(),
+                                          ws.data_ptr(), ws.numel(), _ops.stream(rows)),
+                  "mc_fletcher32_batch")
+    return res.view(torch.uint32).to(torch.int64) if b else res.to(torch.int64)
+
+
+def shuffle_fletcher32_encode_chunks(chunks, elementsize, out=None):
+    """Per chunk: Shuffle(elementsize).encode then Fletcher32.encode, fused.
+
+    Returns a [B, encoded_stride(chunk_bytes)] uint8 tensor; row b holds the
+    chunk_bytes + 4 encoded bytes (the rest of the row is padding).
+    """
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    stride = encoded_stride(n)
+    if out is None:
+        out = torch.empty((b, stride), dtype=torch.uint8, device=rows.device)
+    if b:
+        _native.require_device()
+        with torch.cuda.device(rows.device):
+            ws = _ops.workspace(lib.mc_shuffle_fletcher32_workspace(b, n, elementsize), rows)
+            check(lib.mc_shuffle_fletcher32_encode_batch(
+                rows.data_ptr(), rows.stride(0), out.data_ptr(), out.stride(0), b, n, elementsize,
+                ws.data_ptr(), ws.numel(), _ops.stream(rows)), "mc_shuffle_fletcher32_encode_batch")
+    return out
+
+
+def fletcher32_unshuffle_decode_chunks(encoded, chunk_bytes, elementsize, out=None, check_sums=True):
+    """Per chunk: Fletcher32.decode (verify) then Shuffle(elementsize).decode,
+    fused.  Raises RuntimeError (the reference's message, first bad chunk) on
+    a checksum mismatch when `check_sums`; returns (decoded [B, chunk_bytes],
+    status [B, 2] = (computed, stored))."""
+    rows = _as_rows(encoded)
+    b = rows.shape[0]
+    if out is None:
+        out = torch.empty((b, chunk_bytes), dtype=torch.uint8, device=rows.device)
+    status = torch.empty((b, 2), dtype=torch.int32, device=rows.device)
+    if b:
+        _native.require_device()
+        with torch.cuda.device(rows.device):
+            ws = _ops.workspace(lib.mc_shuffle_fletcher32_workspace(b, chunk_bytes, elementsize), rows)
+            check(lib.mc_fletcher32_unshuffle_batch(
+                rows.data_ptr(), rows.stride(0), out.data_ptr(), out.stride(0), b, chunk_bytes,
+                elementsize, status.data_ptr(), ws.data_ptr(), ws.numel(), _ops.stream(rows)),
+                "mc_fletcher32_unshuffle_batch")
+    if check_sums and b:
+        st = status.view(torch.uint32).to(torch.int64)
+        bad = (st[:, 0] != st[:, 1]).nonzero()
+        if bad.numel():
+            i = int(bad[0, 0])
+            raise _mismatch(int(st[i, 0]), int(st[i, 1]))
+    return out, status
+
+
+class FilterPipeline:
+    """A Zarr-style chain of filters applied in order on encode and in
+    reverse on decode, on device tensors, fusing what it can.
+
+    >>> pipe = FilterPipeline([BitRound(10), Shuffle(4)])        # doctest: +SKIP
+    >>> enc = pipe.encode(x_f32_on_device)                        # doctest: +SKIP
+    """
+
+    def __init__(self, codecs):
+        self.codecs = list(codecs)
+
+    # fusable patterns ------------------------------------------------------
+    @staticmethod
+    def _is_bitround_shuffle(a, b, itemsize):
+        return isinstance(a, BitRound) and isinstance(b, Shuffle) and b.elementsize == itemsize
+
+    def encode(self, buf):
+        x = buf
+        i = 0
+        cs = self.codecs
+        while i < len(cs):
+            c = cs[i]
+            nxt = cs[i + 1] if i + 1 < len(cs) else None
+            if (
+                isinstance(c, BitRound)
+                and is_device_tensor(x)
+                and x.dtype in (torch.float16, torch.float32, torch.float64)
+                and nxt is not None
+                and self._is_bitround_shuffle(c, nxt, x.element_size())
+            ):
+                x = _bitround_shuffle(c, x)
+                i += 2
+                continue
+            if (
+                isinstance(c, Shuffle)
+                and isinstance(nxt, Fletcher32)
+                and is_device_tensor(x)
+                and c.elementsize > 1
+            ):
+                x = _shuffle_fletcher32(c, x)
+                i += 2
+                continue
+            x = c.encode(x)
+            i += 1
+        return x
+
+    def decode(self, buf, out=None):
+        from .compat import ndarray_copy
+
+        x = buf
+        cs = self.codecs[::-1]
+        i = 0
+        while i < len(cs):
+            c = cs[i]
+            nxt = cs[i + 1] if i + 1 < len(cs) else None
+            if (
+                isinstance(c, Fletcher32)
+                and isinstance(nxt, Shuffle)
+                and is_device_tensor(x)
+                and nxt.elementsize > 1
+            ):
+                x = _fletcher32_unshuffle(nxt, x)
+                i += 2
+                continue
+            if i == len(cs) - 1:
+                return c.decode(x, out=out)
+            x = c.decode(x)
+            i += 1
+        return ndarray_copy(x, out)
+
+
+def _bitround_shuffle(br: BitRound, x: torch.Tensor) -> torch.Tensor:
+    from .compat import numpy_dtype
+
+    dt = numpy_dtype(x.dtype)
+    bits = max_bits[str(dt)]
+    if br.keepbits > bits:
+        raise ValueError("Keepbits too large for given dtype")
+    src = x.contiguous().reshape(-1).view(torch.uint8)
+    dst = torch.empty_like(src)
+    _ops.bitround_shuffle(src, dst, src.numel() // dt.itemsize, dt.itemsize, br.keepbits)
+    return dst
+
+
+def _shuffle_fletcher32(sh: Shuffle, x: torch.Tensor) -> torch.Tensor:
+    src = ensure_contiguous_ndarray(x)
+    src = src.view(torch.uint8) if src.numel() else src.new_empty(0, dtype=torch.uint8)
+    n = src.numel()
+    if n == 0:
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    if n % sh.elementsize:
+        raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+    out = torch.empty(n + 4, dtype=torch.uint8, device=src.device)
+    _native.require_device()
+    with torch.cuda.device(src.device):
+        ws = _ops.workspace(lib.mc_shuffle_fletcher32_workspace(1, n, sh.elementsize), src)
+        check(lib.mc_shuffle_fletcher32_encode_batch(src.data_ptr(), n, out.data_ptr(), n + 4, 1, n,
+                                                     sh.elementsize, ws.data_ptr(), ws.numel(),
+                                                     _ops.stream(src)),
+              "mc_shuffle_fletcher32_encode_batch")
+    return out
+
+
+def _fletcher32_unshuffle(sh: Shuffle, x: torch.Tensor) -> torch.Tensor:
+    src = ensure_contiguous_ndarray(x)
+    src = src.view(torch.uint8) if src.numel() else src.new_empty(0, dtype=torch.uint8)
+    if src.numel() <= 4:
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    n = src.numel() - 4
+    if n % sh.elementsize:
+        raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+    out = torch.empty(n, dtype=torch.uint8, device=src.device)
+    status = torch.empty(2, dtype=torch.int32, device=src.device)
+    _native.require_device()
+    with torch.cuda.device(src.device):
+        ws = _ops.workspace(lib.mc_shuffle_fletcher32_workspace(1, n, sh.elementsize), src)
+        check(lib.mc_fletcher32_unshuffle_batch(src.data_ptr(), n + 4, out.data_ptr(), n, 1, n,
+                                                sh.elementsize, status.data_ptr(), ws.data_ptr(),
+                                                ws.numel(), _ops.stream(src)),
+              "mc_fletcher32_unshuffle_batch")
+    v = status.cpu().numpy().view(np.uint32)
+    if v[0] != v[1]:
+        raise _mismatch(int(v[0]), int(v[1]))
+    return out

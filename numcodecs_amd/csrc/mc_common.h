@@ -1,0 +1,338 @@
+// mc_common.h -- shared device/host helpers for libmcodec (gfx950 only).
+//
+// Numeric helpers in this file restate the exact semantics numcodecs inherits
+// from numpy (the arithmetic of bitround.py / delta.py / quantize.py /
+// fixedscaleoffset.py lives in numpy >= 2, pyproject.toml:7,17):
+//   * half <-> float/double conversions follow numpy/_core/src/npymath/halffloat
+//     (npy_float_to_half / npy_double_to_half / npy_half_to_float), bit-exact,
+//     including NaN payloads;
+//   * float -> integer casts follow what numpy's C casts compile to on x86-64
+//     (cvttss2si / cvttsd2si: out-of-range and NaN give the "integer
+//     indefinite" value, then the result is truncated to the target width);
+//   * float16 arithmetic is done in float32 and rounded back to half after each
+//     operation, as numpy's half ufunc loops do.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/mcodec.h"
+
+#define MC_DEV __device__ __forceinline__
+#define MC_HD __host__ __device__ __forceinline__
+
+static inline int mc_hip_status(hipError_t e) {
+  return e == hipSuccess ? MC_OK : (MC_EHIP_BASE - (int)e);
+}
+
+// 16-B vector in a form the nontemporal builtins accept
+typedef uint32_t mc_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t mc_u32x2 __attribute__((ext_vector_type(2)));
+
+// Global streaming accesses.  NT = nontemporal (`nt` bit): measured on MI355X
+// (tools/bwtest.hip, profiles/) a 16-B/lane copy streams at 6.4-6.5 TB/s with
+// nt loads+stores against 5.9 TB/s with default-policy accesses.
+template <bool NT>
+MC_DEV mc_u32x4 mc_ld16(const void *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const mc_u32x4 *>(p));
+  else return *reinterpret_cast<const mc_u32x4 *>(p);
+}
+template <bool NT>
+MC_DEV void mc_st16(void *p, mc_u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<mc_u32x4 *>(p));
+  else *reinterpret_cast<mc_u32x4 *>(p) = v;
+}
+template <bool NT>
+MC_DEV mc_u32x2 mc_ld8(const void *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const mc_u32x2 *>(p));
+  else return *reinterpret_cast<const mc_u32x2 *>(p);
+}
+template <bool NT>
+MC_DEV void mc_st8(void *p, mc_u32x2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<mc_u32x2 *>(p));
+  else *reinterpret_cast<mc_u32x2 *>(p) = v;
+}
+template <bool NT>
+MC_DEV uint32_t mc_ld4(const void *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p));
+  else return *reinterpret_cast<const uint32_t *>(p);
+}
+template <bool NT>
+MC_DEV void mc_st4(void *p, uint32_t v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(p));
+  else *reinterpret_cast<uint32_t *>(p) = v;
+}
+
+// launch-error check after a <<<>>> launch
+static inline int mc_last_launch() { return mc_hip_status(hipGetLastError()); }
+
+static constexpr int MC_BLOCK = 256;  // 4 waves of 64 lanes
+
+// grid cap for grid-stride streaming kernels: 256 CUs x 8 blocks of 256 threads
+static constexpr unsigned MC_MAX_GRID = 256u * 8u;
+
+static inline unsigned mc_grid_for(size_t work_items, size_t per_block,
+                                   unsigned cap = MC_MAX_GRID) {
+  size_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---------------------------------------------------------------------------
+// dtype table
+// ---------------------------------------------------------------------------
+MC_HD int mc_itemsize(int dt) {
+  switch (dt) {
+    case MC_B1: case MC_I1: case MC_U1: return 1;
+    case MC_I2: case MC_U2: case MC_F2: return 2;
+    case MC_I4: case MC_U4: case MC_F4: return 4;
+    case MC_I8: case MC_U8: case MC_F8: return 8;
+    default: return 0;
+  }
+}
+MC_HD bool mc_is_float(int dt) { return dt == MC_F2 || dt == MC_F4 || dt == MC_F8; }
+MC_HD bool mc_is_signed(int dt) {
+  return dt == MC_I1 || dt == MC_I2 || dt == MC_I4 || dt == MC_I8;
+}
+static inline bool mc_valid_dtype(int dt) { return dt >= 0 && dt < MC_NDTYPES; }
+
+// ---------------------------------------------------------------------------
+// byte transposes (v_perm_b32).  perm(hi, lo, sel): byte k of the result is
+// byte sel[8k+7:8k] of the 8-byte value {hi:lo} (lo = bytes 0-3).
+// ---------------------------------------------------------------------------
+MC_DEV uint32_t mc_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// 4x4 byte transpose: p_b byte j = d_j byte b.  It is its own inverse.
+MC_DEV void mc_tr4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3,
+                   uint32_t &p0, uint32_t &p1, uint32_t &p2, uint32_t &p3) {
+  const uint32_t a0 = mc_perm(d1, d0, 0x05010400u);  // d0b0 d1b0 d0b1 d1b1
+  const uint32_t a1 = mc_perm(d1, d0, 0x07030602u);  // d0b2 d1b2 d0b3 d1b3
+  const uint32_t a2 = mc_perm(d3, d2, 0x05010400u);  // d2b0 d3b0 d2b1 d3b1
+  const uint32_t a3 = mc_perm(d3, d2, 0x07030602u);  // d2b2 d3b2 d2b3 d3b3
+  p0 = mc_perm(a2, a0, 0x05040100u);
+  p1 = mc_perm(a2, a0, 0x07060302u);
+  p2 = mc_perm(a3, a1, 0x05040100u);
+  p3 = mc_perm(a3, a1, 0x07060302u);
+}
+
+// A "quad" is 4 consecutive elements of ES bytes = ES dwords in memory order.
+// Its plane form is ES dwords: plane b holds byte b of the 4 elements.
+template <int ES>
+MC_DEV void mc_quad_to_planes(const uint32_t (&w)[ES], uint32_t (&p)[ES]) {
+  if constexpr (ES == 2) {
+    p[0] = mc_perm(w[1], w[0], 0x06040200u);
+    p[1] = mc_perm(w[1], w[0], 0x07050301u);
+  } else {
+    static_assert(ES % 4 == 0, "ES must be 2 or a multiple of 4");
+    constexpr int C = ES / 4;  // dwords per element
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      mc_tr4(w[c], w[C + c], w[2 * C + c], w[3 * C + c], p[4 * c], p[4 * c + 1],
+             p[4 * c + 2], p[4 * c + 3]);
+  }
+}
+
+template <int ES>
+MC_DEV void mc_planes_to_quad(const uint32_t (&p)[ES], uint32_t (&w)[ES]) {
+  if constexpr (ES == 2) {
+    w[0] = mc_perm(p[1], p[0], 0x05010400u);
+    w[1] = mc_perm(p[1], p[0], 0x07030602u);
+  } else {
+    constexpr int C = ES / 4;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      mc_tr4(p[4 * c], p[4 * c + 1], p[4 * c + 2], p[4 * c + 3], w[c], w[C + c],
+             w[2 * C + c], w[3 * C + c]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BitRound on the integer view (bitround.py:62-68):
+//   b += ((b >> maskbits) & 1) + half_quantum1 ; b &= mask
+// with wrap-around in the same-width signed integer.
+// ---------------------------------------------------------------------------
+struct McBitRound {
+  uint64_t mask;   // (-1 >> maskbits) << maskbits, in the element width
+  uint64_t half;   // (1 << (maskbits-1)) - 1
+  int maskbits;
+};
+
+static inline McBitRound mc_make_bitround(int itemsize, int keepbits) {
+  const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
+  McBitRound br;
+  br.maskbits = mbits - keepbits;
+  br.mask = ~0ull << br.maskbits;
+  br.half = (1ull << (br.maskbits - 1)) - 1ull;
+  return br;
+}
+
+MC_DEV uint32_t mc_bitround32(uint32_t b, const McBitRound &br) {
+  b += ((b >> br.maskbits) & 1u) + (uint32_t)br.half;
+  return b & (uint32_t)br.mask;
+}
+MC_DEV uint32_t mc_bitround16x2(uint32_t w, const McBitRound &br) {
+  // two independent 16-bit lanes in one dword
+  uint32_t lo = w & 0xffffu, hi = w >> 16;
+  lo = (lo + ((lo >> br.maskbits) & 1u) + (uint32_t)br.half) & (uint32_t)br.mask & 0xffffu;
+  hi = (hi + ((hi >> br.maskbits) & 1u) + (uint32_t)br.half) & (uint32_t)br.mask & 0xffffu;
+  return lo | (hi << 16);
+}
+MC_DEV uint64_t mc_bitround64(uint64_t b, const McBitRound &br) {
+  b += ((b >> br.maskbits) & 1ull) + br.half;
+  return b & br.mask;
+}
+
+// apply BitRound to the elements of a quad (ES dwords)
+template <int ES>
+MC_DEV void mc_bitround_quad(uint32_t (&w)[ES], const McBitRound &br) {
+  if constexpr (ES == 2) {
+    w[0] = mc_bitround16x2(w[0], br);
+    w[1] = mc_bitround16x2(w[1], br);
+  } else if constexpr (ES == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = mc_bitround32(w[j], br);
+  } else if constexpr (ES == 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint64_t v = ((uint64_t)w[2 * j + 1] << 32) | w[2 * j];
+      v = mc_bitround64(v, br);
+      w[2 * j] = (uint32_t)v;
+      w[2 * j + 1] = (uint32_t)(v >> 32);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// numpy half-float conversions (npymath/halffloat.cpp), bit-exact.
+// ---------------------------------------------------------------------------
+MC_HD uint16_t mc_float_bits_to_half(uint32_t f) {
+  uint32_t f_exp, f_sig;
+  uint16_t h_sgn, h_exp, h_sig;
+  h_sgn = (uint16_t)((f & 0x80000000u) >> 16);
+  f_exp = (f & 0x7f800000u);
+  if (f_exp >= 0x47800000u) {                  // overflow, inf or NaN
+    if (f_exp == 0x7f800000u) {
+      f_sig = (f & 0x007fffffu);
+      if (f_sig != 0) {                         // NaN: keep upper payload bits
+        uint16_t ret = (uint16_t)(0x7c00u + (f_sig >> 13));
+        if (ret == 0x7c00u) ret++;              // do not turn a NaN into inf
+        return (uint16_t)(h_sgn + ret);
+      }
+      return (uint16_t)(h_sgn + 0x7c00u);      // inf
+    }
+    return (uint16_t)(h_sgn + 0x7c00u);        // overflow to inf
+  }
+  if (f_exp <= 0x38000000u) {                  // subnormal or zero half
+    if (f_exp < 0x33000000u) return h_sgn;     // underflow to signed zero
+    f_exp >>= 23;
+    f_sig = (0x00800000u + (f & 0x007fffffu));
+    // round to nearest even at the half-subnormal lsb (2^-24)
+    const uint32_t shift = 126 - f_exp;  // 14..24
+    uint32_t sig = f_sig >> (shift - 1);  // keep one extra (guard) bit
+    const bool sticky = (f_sig & ((1u << (shift - 1)) - 1u)) != 0;
+    const bool guard = sig & 1u;
+    sig >>= 1;
+    if (guard && (sticky || (sig & 1u))) sig += 1;
+    h_sig = (uint16_t)sig;
+    return (uint16_t)(h_sgn + h_sig);
+  }
+  // normal half
+  h_exp = (uint16_t)((f_exp - 0x38000000u) >> 13);
+  f_sig = (f & 0x007fffffu);
+  // round to nearest even on bit 13 (a tie with an even lsb stays)
+  if ((f_sig & 0x00003fffu) != 0x00001000u) {
+    f_sig += 0x00001000u;
+  }
+  h_sig = (uint16_t)(f_sig >> 13);
+  // carry from the significand rounding bumps the exponent (may give inf)
+  return (uint16_t)(h_sgn + (uint16_t)(h_exp + h_sig));
+}
+
+MC_HD uint16_t mc_double_bits_to_half(uint64_t d) {
+  uint64_t d_exp, d_sig;
+  uint16_t h_sgn, h_exp, h_sig;
+  h_sgn = (uint16_t)((d & 0x8000000000000000ull) >> 48);
+  d_exp = (d & 0x7ff0000000000000ull);
+  if (d_exp >= 0x40f0000000000000ull) {
+    if (d_exp == 0x7ff0000000000000ull) {
+      d_sig = (d & 0x000fffffffffffffull);
+      if (d_sig != 0) {
+        uint16_t ret = (uint16_t)(0x7c00u + (d_sig >> 42));
+        if (ret == 0x7c00u) ret++;
+        return (uint16_t)(h_sgn + ret);
+      }
+      return (uint16_t)(h_sgn + 0x7c00u);
+    }
+    return (uint16_t)(h_sgn + 0x7c00u);
+  }
+  if (d_exp <= 0x3f00000000000000ull) {
+    if (d_exp < 0x3e60000000000000ull) return h_sgn;
+    d_exp >>= 52;
+    d_sig = (0x0010000000000000ull + (d & 0x000fffffffffffffull));
+    const uint64_t shift = 1051 - d_exp;  // 43..53 (to the half subnormal lsb)
+    uint64_t sig = d_sig >> (shift - 1);
+    const bool sticky = (d_sig & ((1ull << (shift - 1)) - 1ull)) != 0;
+    const bool guard = sig & 1ull;
+    sig >>= 1;
+    if (guard && (sticky || (sig & 1ull))) sig += 1;
+    h_sig = (uint16_t)sig;
+    return (uint16_t)(h_sgn + h_sig);
+  }
+  h_exp = (uint16_t)((d_exp - 0x3f00000000000000ull) >> 42);
+  d_sig = (d & 0x000fffffffffffffull);
+  if ((d_sig & 0x000007ffffffffffull) != 0x0000020000000000ull) {
+    d_sig += 0x0000020000000000ull;
+  }
+  h_sig = (uint16_t)(d_sig >> 42);
+  return (uint16_t)(h_sgn + (uint16_t)(h_exp + h_sig));
+}
+
+MC_HD uint32_t mc_half_to_float_bits(uint16_t h) {
+  uint16_t h_exp = (h & 0x7c00u);
+  uint32_t f_sgn = ((uint32_t)h & 0x8000u) << 16;
+  switch (h_exp) {
+    case 0x0000u: {  // zero or subnormal
+      uint16_t h_sig = (h & 0x03ffu);
+      if (h_sig == 0) return f_sgn;
+      h_sig <<= 1;
+      uint32_t f_exp;
+      int k = 0;
+      while ((h_sig & 0x0400u) == 0) { h_sig <<= 1; ++k; }
+      f_exp = ((uint32_t)(127 - 15 - k)) << 23;
+      uint32_t f_sig = ((uint32_t)(h_sig & 0x03ffu)) << 13;
+      return f_sgn + f_exp + f_sig;
+    }
+    case 0x7c00u:  // inf or NaN: all-ones exponent, keep the significand
+      return f_sgn + 0x7f800000u + (((uint32_t)(h & 0x03ffu)) << 13);
+    default:  // normalised: just shift the exponent and significand
+      return f_sgn + (((uint32_t)(h & 0x7fffu) + 0x1c000u) << 13);
+  }
+}
+
+MC_HD float mc_bits_f32(uint32_t b) { return __builtin_bit_cast(float, b); }
+MC_HD uint32_t mc_f32_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
+MC_HD double mc_bits_f64(uint64_t b) { return __builtin_bit_cast(double, b); }
+MC_HD uint64_t mc_f64_bits(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+MC_HD float mc_half_to_float(uint16_t h) { return mc_bits_f32(mc_half_to_float_bits(h)); }
+MC_HD uint16_t mc_float_to_half(float f) { return mc_float_bits_to_half(mc_f32_bits(f)); }
+MC_HD uint16_t mc_double_to_half(double d) { return mc_double_bits_to_half(mc_f64_bits(d)); }
+
+// ---------------------------------------------------------------------------
+// x86-64 float -> integer casts, as numpy's `(npy_T)x` compiles with gcc.
+// ---------------------------------------------------------------------------
+MC_HD int32_t mc_cvtt_i32(double x) {  // cvttss2si/cvttsd2si eax
+  return (x > -2147483649.0 && x < 2147483648.0) ? (int32_t)x : INT32_MIN;
+}
+MC_HD int64_t mc_cvtt_i64(double x) {  // cvttsd2si rax
+  return (x >= -9223372036854775808.0 && x < 9223372036854775808.0) ? (int64_t)x
+                                                                     : INT64_MIN;
+}
+MC_HD uint64_t mc_cvtt_u64(double x) {  // gcc's unsigned sequence (no AVX-512)
+  if (!(x >= 9223372036854775808.0)) return (uint64_t)mc_cvtt_i64(x);
+  return (uint64_t)mc_cvtt_i64(x - 9223372036854775808.0) ^ 0x8000000000000000ull;
+}

@@ -1,0 +1,314 @@
+// mc_elementwise.hip -- fused per-element codecs for gfx950.
+//
+//   mc_bitround   bitround.py:45-69   (integer ops on the same-width view)
+//   mc_fso_encode fixedscaleoffset.py:83-97   astype(rint((x - offset) * scale))
+//   mc_fso_decode fixedscaleoffset.py:99-113  dtype(x / scale + offset)
+//   mc_quantize   quantize.py:60-76   astype(rint(scale * x) / scale)
+//   mc_cast       ndarray.astype (quantize.py:80, compat.py:177-206)
+//   mc_delta_encode delta.py:52-67     x[0], np.diff(x)
+//
+// Each numpy expression of the reference is one pass over HBM here (the
+// reference makes 2-5 full-array temporaries).  Lanes move 4 consecutive
+// elements per step with one vector access (lane-contiguous across the wave);
+// a thread does STEPS steps, so a workgroup covers 4*STEPS*256 elements and
+// the grid covers the whole array (no grid-stride loop: see mc_shuffle.hip on
+// why looping workgroups lose to one-tile-per-workgroup).  Scalars arrive
+// already converted to their compute dtype by the host (NEP 50 rules).
+#include "mc_num.h"
+
+namespace {
+
+constexpr int STEPS = 4;
+constexpr int ELEMS_PER_BLOCK = 4 * STEPS * MC_BLOCK;  // 4096
+
+enum MapKind { K_CAST = 0, K_FSO_ENC = 1, K_FSO_DEC = 2, K_QUANTIZE = 3 };
+
+struct MapParams {
+  int d, t1, t2, a;  // input dtype, compute dtypes, output dtype
+  McNum s0, s1;      // scalars in their compute dtypes
+};
+
+template <int KIND>
+MC_DEV McNum map_op(McNum x, int d, int t1, int t2, int a, const McNum &s0, const McNum &s1) {
+  if constexpr (KIND == K_CAST) {
+    return mc_num_cast(x, d, a);
+  } else if constexpr (KIND == K_FSO_ENC) {  // s0 = offset (t1), s1 = scale (t2)
+    McNum v = mc_num_cast(x, d, t1);
+    v = mc_num_binop(v, s0, MC_OP_SUB, t1);
+    v = mc_num_cast(v, t1, t2);
+    v = mc_num_binop(v, s1, MC_OP_MUL, t2);
+    v = mc_num_rint(v, t2);
+    return mc_num_cast(v, t2, a);
+  } else if constexpr (KIND == K_FSO_DEC) {  // s0 = scale (t1), s1 = offset (t2)
+    McNum v = mc_num_cast(x, d, t1);
+    v = mc_num_binop(v, s0, MC_OP_DIV, t1);
+    v = mc_num_cast(v, t1, t2);
+    v = mc_num_binop(v, s1, MC_OP_ADD, t2);
+    return mc_num_cast(v, t2, a);
+  } else {  // K_QUANTIZE: s0 = scale (d)
+    McNum v = mc_num_cast(x, d, d);
+    v = mc_num_binop(s0, v, MC_OP_MUL, d);
+    v = mc_num_rint(v, d);
+    v = mc_num_binop(v, s0, MC_OP_DIV, d);
+    return mc_num_cast(v, d, a);
+  }
+}
+
+// D_/T1_/T2_/A_ >= 0: compile-time dtypes (specialised hot paths); -1: runtime.
+template <int KIND, int D_, int T1_, int T2_, int A_, bool VEC>
+__global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ src,
+                                                  uint8_t *__restrict__ dst, size_t n,
+                                                  MapParams prm) {
+  const int d = D_ >= 0 ? D_ : prm.d;
+  const int t1 = T1_ >= 0 ? T1_ : prm.t1;
+  const int t2 = T2_ >= 0 ? T2_ : prm.t2;
+  const int a = A_ >= 0 ? A_ : prm.a;
+  const int ss = mc_itemsize(d), ds = mc_itemsize(a);
+  const size_t base = (size_t)blockIdx.x * ELEMS_PER_BLOCK;
+  if constexpr (VEC) {
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const size_t i0 = base + (size_t)s * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
+      if (i0 + 4 <= n) {
+        uint64_t e[4], o[4];
+        mc_load4(src + i0 * ss, ss, e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          o[k] = mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e[k], d), d, t1, t2, a, prm.s0, prm.s1), a);
+        mc_store4(dst + i0 * ds, ds, o);
+      } else {
+        for (size_t i = i0; i < n; ++i)
+          mc_store_elem(dst, i, ds,
+                        mc_num_to_bits(map_op<KIND>(mc_num_from_bits(mc_load_elem(src, i, ss), d),
+                                                    d, t1, t2, a, prm.s0, prm.s1), a));
+      }
+    }
+  } else {
+    for (size_t i = base + threadIdx.x; i < n && i < base + ELEMS_PER_BLOCK; i += MC_BLOCK)
+      mc_store_elem_u(dst, i, ds,
+                      mc_num_to_bits(map_op<KIND>(mc_num_from_bits(mc_load_elem_u(src, i, ss), d),
+                                                  d, t1, t2, a, prm.s0, prm.s1), a));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BitRound (bitround.py:62-68) on 16-B vectors
+// ---------------------------------------------------------------------------
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_bitround(const uint8_t *__restrict__ src,
+                                                       uint8_t *__restrict__ dst, size_t nbytes,
+                                                       McBitRound br, bool vec) {
+  const size_t base = (size_t)blockIdx.x * (16 * STEPS * MC_BLOCK);
+  if (vec) {
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const size_t o = base + ((size_t)s * MC_BLOCK + threadIdx.x) * 16;
+      if (o + 16 <= nbytes) {
+        mc_u32x4 v = mc_ld16<true>(src + o);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        if constexpr (ES == 2) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) w[k] = mc_bitround16x2(w[k], br);
+        } else if constexpr (ES == 4) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) w[k] = mc_bitround32(w[k], br);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const uint64_t r = mc_bitround64(((uint64_t)w[2 * k + 1] << 32) | w[2 * k], br);
+            w[2 * k] = (uint32_t)r;
+            w[2 * k + 1] = (uint32_t)(r >> 32);
+          }
+        }
+        mc_st16<true>(dst + o, mc_u32x4{w[0], w[1], w[2], w[3]});
+      } else if (o < nbytes) {  // tail: whole elements, byte-wise
+        for (size_t e = o; e + ES <= nbytes; e += ES) {
+          uint64_t v = mc_load_elem_u(src + e, 0, ES);
+          v = ES == 2 ? (mc_bitround16x2((uint32_t)v, br) & 0xffffu)
+              : ES == 4 ? mc_bitround32((uint32_t)v, br) : mc_bitround64(v, br);
+          mc_store_elem_u(dst + e, 0, ES, v);
+        }
+      }
+    }
+  } else {
+    const size_t per = 16 * STEPS * MC_BLOCK;
+    for (size_t e = base + (size_t)threadIdx.x * ES; e + ES <= nbytes && e < base + per;
+         e += (size_t)MC_BLOCK * ES) {
+      uint64_t v = mc_load_elem_u(src + e, 0, ES);
+      v = ES == 2 ? (mc_bitround16x2((uint32_t)v, br) & 0xffffu)
+          : ES == 4 ? mc_bitround32((uint32_t)v, br) : mc_bitround64(v, br);
+      mc_store_elem_u(dst + e, 0, ES, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Delta encode (delta.py:52-67): y[0] = astype(x[0]); y[i] = astype(x[i] - x[i-1])
+// with the difference computed in dtype (bool: not_equal, as np.diff does).
+// ---------------------------------------------------------------------------
+template <int D_, int A_, bool VEC>
+__global__ __launch_bounds__(MC_BLOCK) void k_delta_enc(const uint8_t *__restrict__ src,
+                                                        uint8_t *__restrict__ dst, size_t n,
+                                                        int d_rt, int a_rt) {
+  const int d = D_ >= 0 ? D_ : d_rt;
+  const int a = A_ >= 0 ? A_ : a_rt;
+  const int ss = mc_itemsize(d), ds = mc_itemsize(a);
+  const size_t base = (size_t)blockIdx.x * ELEMS_PER_BLOCK;
+  auto diff = [&](McNum cur, McNum prev) {
+    return mc_num_cast(mc_num_binop(cur, prev, MC_OP_SUB, d), d, a);
+  };
+  if constexpr (VEC) {
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const size_t i0 = base + (size_t)s * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
+      if (i0 + 4 <= n) {
+        uint64_t e[4], o[4];
+        mc_load4(src + i0 * ss, ss, e);
+        McNum x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = mc_num_from_bits(e[k], d);
+        const McNum prev = i0 ? mc_num_from_bits(mc_load_elem(src, i0 - 1, ss), d) : x[0];
+        o[0] = mc_num_to_bits(i0 ? diff(x[0], prev) : mc_num_cast(x[0], d, a), a);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) o[k] = mc_num_to_bits(diff(x[k], x[k - 1]), a);
+        mc_store4(dst + i0 * ds, ds, o);
+      } else {
+        for (size_t i = i0; i < n; ++i) {
+          const McNum x = mc_num_from_bits(mc_load_elem(src, i, ss), d);
+          const McNum r = i ? diff(x, mc_num_from_bits(mc_load_elem(src, i - 1, ss), d))
+                            : mc_num_cast(x, d, a);
+          mc_store_elem(dst, i, ds, mc_num_to_bits(r, a));
+        }
+      }
+    }
+  } else {
+    for (size_t i = base + threadIdx.x; i < n && i < base + ELEMS_PER_BLOCK; i += MC_BLOCK) {
+      const McNum x = mc_num_from_bits(mc_load_elem_u(src, i, ss), d);
+      const McNum r = i ? diff(x, mc_num_from_bits(mc_load_elem_u(src, i - 1, ss), d))
+                        : mc_num_cast(x, d, a);
+      mc_store_elem_u(dst, i, ds, mc_num_to_bits(r, a));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host dispatch
+// ---------------------------------------------------------------------------
+static bool aligned_for(const void *p, int itemsize) {
+  return ((uintptr_t)p % (uintptr_t)(4 * itemsize)) == 0;
+}
+
+static unsigned blocks_for(size_t n) {
+  return (unsigned)((n + ELEMS_PER_BLOCK - 1) / ELEMS_PER_BLOCK);
+}
+
+template <int KIND>
+static int launch_map(const void *src, void *dst, size_t n, const MapParams &p, hipStream_t st) {
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  if (!mc_valid_dtype(p.d) || !mc_valid_dtype(p.t1) || !mc_valid_dtype(p.t2) || !mc_valid_dtype(p.a))
+    return MC_EINVAL;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const bool vec = aligned_for(src, mc_itemsize(p.d)) && aligned_for(dst, mc_itemsize(p.a));
+  const unsigned grid = blocks_for(n);
+  // specialised hot paths (constant dtypes): C4's FSO f4 -> i2 and i2 -> f4
+  if (KIND == K_FSO_ENC && vec && p.d == MC_F4 && p.t1 == MC_F4 && p.t2 == MC_F4 && p.a == MC_I2) {
+    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (KIND == K_FSO_DEC && vec && p.d == MC_I2 && p.t1 == MC_F8 && p.t2 == MC_F8 &&
+             p.a == MC_F4) {
+    k_map<KIND, MC_I2, MC_F8, MC_F8, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (KIND == K_QUANTIZE && vec && p.d == MC_F4 && p.a == MC_F4) {
+    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (vec) {
+    k_map<KIND, -1, -1, -1, -1, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else {
+    k_map<KIND, -1, -1, -1, -1, false><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  }
+  return mc_last_launch();
+}
+
+static McNum num_scalar(int dt, double f, int64_t i) {
+  McNum r;
+  r.f = mc_is_float(dt) ? f : 0.0;
+  r.i = mc_is_float(dt) ? 0 : i;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_bitround(const void *src, void *dst, size_t n, int itemsize, int keepbits,
+                mc_stream_t stream) {
+  if (!(itemsize == 2 || itemsize == 4 || itemsize == 8)) return MC_EINVAL;
+  const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
+  if (keepbits < 0 || keepbits > mbits) return MC_EINVAL;
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t nbytes = n * (size_t)itemsize;
+  if (keepbits == mbits)
+    return mc_hip_status(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, st));
+  const McBitRound br = mc_make_bitround(itemsize, keepbits);
+  const bool vec = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  const size_t per = 16 * STEPS * MC_BLOCK;
+  const unsigned grid = (unsigned)((nbytes + per - 1) / per);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  switch (itemsize) {
+    case 2: k_bitround<2><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, br, vec); break;
+    case 4: k_bitround<4><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, br, vec); break;
+    default: k_bitround<8><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, br, vec); break;
+  }
+  return mc_last_launch();
+}
+
+int mc_cast(const void *src, void *dst, size_t n, int from_dtype, int to_dtype,
+            mc_stream_t stream) {
+  MapParams p{from_dtype, from_dtype, from_dtype, to_dtype, McNum{0, 0}, McNum{0, 0}};
+  return launch_map<K_CAST>(src, dst, n, p, (hipStream_t)stream);
+}
+
+int mc_fso_encode(const void *src, void *dst, size_t n, int dtype, int t1, int t2, int astype,
+                  double offset_f, int64_t offset_i, double scale_f, int64_t scale_i,
+                  mc_stream_t stream) {
+  MapParams p{dtype, t1, t2, astype, num_scalar(t1, offset_f, offset_i),
+              num_scalar(t2, scale_f, scale_i)};
+  return launch_map<K_FSO_ENC>(src, dst, n, p, (hipStream_t)stream);
+}
+
+int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3, int t4, int dtype,
+                  double scale, double offset, mc_stream_t stream) {
+  if (!mc_is_float(t3) || !mc_is_float(t4)) return MC_EINVAL;
+  MapParams p{astype, t3, t4, dtype, num_scalar(t3, scale, 0), num_scalar(t4, offset, 0)};
+  return launch_map<K_FSO_DEC>(src, dst, n, p, (hipStream_t)stream);
+}
+
+int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, double scale,
+                mc_stream_t stream) {
+  if (!mc_is_float(dtype) || !mc_is_float(astype)) return MC_EINVAL;
+  MapParams p{dtype, dtype, dtype, astype, num_scalar(dtype, scale, 0), McNum{0, 0}};
+  return launch_map<K_QUANTIZE>(src, dst, n, p, (hipStream_t)stream);
+}
+
+int mc_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype,
+                    mc_stream_t stream) {
+  if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const bool vec = aligned_for(src, mc_itemsize(dtype)) && aligned_for(dst, mc_itemsize(astype));
+  const unsigned grid = blocks_for(n);
+  if (vec && dtype == MC_I2 && astype == MC_I2)
+    k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
+  else if (vec)
+    k_delta_enc<-1, -1, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
+  else
+    k_delta_enc<-1, -1, false><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
+  return mc_last_launch();
+}
+
+}  // extern "C"

@@ -1,0 +1,505 @@
+// mc_fletcher.hip -- Fletcher32 (fletcher32.pyx:24-115) for gfx950, alone and
+// fused with Shuffle over batches of chunks.
+//
+// The reference loop (HDF5 H5checksum.c) adds big-endian 16-bit words,
+// sum1 += w; sum2 += sum1, folding both sums every 360 words with
+// x = (x & 0xffff) + (x >> 16) and twice at the end.  Folding preserves the
+// value mod 65535 and never turns a positive sum into 0, and the 360-word
+// blocks keep the uint32 sums from overflowing, so with n = ceil(len/2) words
+// (an odd trailing byte is the high byte of a last word):
+//     S1 = sum_i w_i,   S2 = sum_i (n - i) * w_i
+//     result = (r(S2) << 16) | r(S1),  r(S) = 0 if S == 0 else ((S-1) mod 65535) + 1
+// and S == 0 exactly when every word is zero.  With absolute weights (n - i)
+// any partition of the words into slices adds up mod 65535, which makes the
+// checksum a plain parallel reduction: lanes accumulate 16-B vectors (8 words)
+// as S1 += A, S2 += c*A - B with A = sum w_m, B = sum m*w_m, c = (n - j0) mod
+// 65535; workgroups reduce through wave shuffles and LDS; partials per
+// (chunk, slice) are folded by a small finalize kernel that also writes the
+// little-endian footer (_utils.pxd:11-24) or compares against it.
+#include "mc_shuffle.h"
+
+namespace {
+
+constexpr uint32_t M = 65535u;
+
+struct F32Part {
+  uint64_t s1;   // sum of words
+  uint64_t s2a;  // sum of c * A
+  uint64_t s2b;  // sum of B (intra-vector weights)
+  uint32_t nz;   // OR of all words
+};
+
+MC_DEV void part_init(F32Part &p) { p.s1 = p.s2a = p.s2b = 0; p.nz = 0; }
+
+// the two big-endian words of a little-endian dword: w0 = bytes(0,1), w1 = bytes(2,3)
+MC_DEV uint32_t be_swap16x2(uint32_t x) { return mc_perm(0u, x, 0x02030001u); }
+
+// 16-B vector whose first word has weight c (= (n - j0) mod M)
+MC_DEV void part_vec(F32Part &p, mc_u32x4 v, uint32_t c) {
+  const uint32_t y0 = be_swap16x2(v.x), y1 = be_swap16x2(v.y);
+  const uint32_t y2 = be_swap16x2(v.z), y3 = be_swap16x2(v.w);
+  const uint32_t w0 = y0 & 0xffffu, w1 = y0 >> 16, w2 = y1 & 0xffffu, w3 = y1 >> 16;
+  const uint32_t w4 = y2 & 0xffffu, w5 = y2 >> 16, w6 = y3 & 0xffffu, w7 = y3 >> 16;
+  const uint32_t A = w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
+  const uint32_t B = w1 + 2 * w2 + 3 * w3 + 4 * w4 + 5 * w5 + 6 * w6 + 7 * w7;
+  p.s1 += A;
+  p.s2a += (uint64_t)c * A;
+  p.s2b += B;
+  p.nz |= v.x | v.y | v.z | v.w;
+}
+
+// one dword (two words) whose first word has weight c
+MC_DEV void part_dword(F32Part &p, uint32_t x, uint32_t c) {
+  const uint32_t y = be_swap16x2(x);
+  const uint32_t w0 = y & 0xffffu, w1 = y >> 16;
+  p.s1 += w0 + w1;
+  p.s2a += (uint64_t)c * (w0 + w1);
+  p.s2b += w1;
+  p.nz |= x;
+}
+
+// one word with weight c
+MC_DEV void part_word(F32Part &p, uint32_t w, uint32_t c) {
+  p.s1 += w;
+  p.s2a += (uint64_t)c * w;
+  p.nz |= w;
+}
+
+MC_DEV uint32_t mod_m(uint64_t x) { return (uint32_t)(x % M); }
+
+// reduce a thread's partial to {S1 mod M, S2 mod M, nz} across the block;
+// valid in thread 0.
+MC_DEV void block_reduce(const F32Part &p, uint32_t &s1, uint32_t &s2, uint32_t &nz) {
+  __shared__ uint32_t red[3][MC_BLOCK / 64];
+  uint64_t a = mod_m(p.s1);
+  uint64_t b = (mod_m(p.s2a) + M - mod_m(p.s2b)) % M;
+  uint32_t z = p.nz;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_down(a, off, 64);
+    b += __shfl_down(b, off, 64);
+    z |= __shfl_down(z, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = mod_m(a);
+    red[1][wave] = mod_m(b);
+    red[2][wave] = z;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t x = 0, y = 0;
+    uint32_t q = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) {
+      x += red[0][w];
+      y += red[1][w];
+      q |= red[2][w];
+    }
+    s1 = mod_m(x);
+    s2 = mod_m(y);
+    nz = q;
+  }
+}
+
+MC_DEV uint32_t final_sum(uint32_t s1, uint32_t s2, uint32_t nz) {
+  if (!nz) return 0u;
+  const uint32_t r1 = (s1 + M - 1) % M + 1, r2 = (s2 + M - 1) % M + 1;
+  return (r2 << 16) | r1;
+}
+
+MC_DEV void store_le32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+MC_DEV uint32_t load_le32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// ---------------------------------------------------------------------------
+// checksum (optionally fused with a copy) over slices of chunks
+// block = (chunk c, slice sl); partials[block] = {S1, S2, nz}
+// ---------------------------------------------------------------------------
+template <bool COPY, bool VEC>
+__global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
+    const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
+    size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials) {
+  const size_t c = blockIdx.x / nslices;
+  const unsigned sl = blockIdx.x - (unsigned)(c * nslices);
+  const uint8_t *s = src + c * src_stride;
+  uint8_t *d = COPY ? dst + c * dst_stride : nullptr;
+  const uint64_t nwords = (nbytes + 1) / 2;
+  const size_t nvec = VEC ? nbytes / 16 : 0;
+  const size_t v_lo = nvec * sl / nslices, v_hi = nvec * (sl + 1) / nslices;
+  F32Part p;
+  part_init(p);
+  {
+    size_t v = v_lo + threadIdx.x;
+    // weight of the vector's first word, stepped by 8*MC_BLOCK words per iteration
+    uint32_t cw = (uint32_t)((nwords - 8 * (uint64_t)v) % M);
+    constexpr uint32_t STEP = (8u * MC_BLOCK) % M;
+    for (; v < v_hi; v += MC_BLOCK) {
+      const mc_u32x4 x = mc_ld16<true>(s + v * 16);
+      if constexpr (COPY) mc_st16<true>(d + v * 16, x);
+      part_vec(p, x, cw);
+      cw = cw >= STEP ? cw - STEP : cw + M - STEP;
+    }
+  }
+  if (sl == nslices - 1) {  // bytes after the last whole vector, word by word
+    const size_t b0 = nvec * 16;
+    for (size_t b = b0 + 2 * (size_t)threadIdx.x; b < nbytes; b += 2 * MC_BLOCK) {
+      const uint32_t hi = s[b];
+      const uint32_t lo = b + 1 < nbytes ? s[b + 1] : 0u;
+      if constexpr (COPY) {
+        d[b] = (uint8_t)hi;
+        if (b + 1 < nbytes) d[b + 1] = (uint8_t)lo;
+      }
+      part_word(p, (hi << 8) | lo, (uint32_t)((nwords - b / 2) % M));
+    }
+  }
+  uint32_t s1, s2, nz;
+  block_reduce(p, s1, s2, nz);
+  if (threadIdx.x == 0) {
+    partials[3 * (size_t)blockIdx.x + 0] = s1;
+    partials[3 * (size_t)blockIdx.x + 1] = s2;
+    partials[3 * (size_t)blockIdx.x + 2] = nz;
+  }
+}
+
+enum FinalMode { F_SUM = 0, F_FOOTER = 1, F_VERIFY = 2 };
+
+// one thread per chunk: fold the chunk's slices, then
+//   F_SUM:    out[c] = checksum
+//   F_FOOTER: LE32 checksum at dst + c*dst_stride + nbytes (and out[c] if set)
+//   F_VERIFY: out[2c] = checksum, out[2c+1] = LE32 footer at src + c*src_stride + nbytes
+__global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
+    const uint32_t *__restrict__ partials, unsigned nslices, size_t nchunks, int mode,
+    const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
+    size_t dst_stride, size_t nbytes, uint32_t *__restrict__ out) {
+  const size_t c = (size_t)blockIdx.x * MC_BLOCK + threadIdx.x;
+  if (c >= nchunks) return;
+  uint64_t a = 0, b = 0;
+  uint32_t z = 0;
+  for (unsigned sl = 0; sl < nslices; ++sl) {
+    const uint32_t *q = partials + 3 * (c * nslices + sl);
+    a += q[0];
+    b += q[1];
+    z |= q[2];
+  }
+  const uint32_t f = final_sum(mod_m(a), mod_m(b), z);
+  if (mode == F_SUM) {
+    out[c] = f;
+  } else if (mode == F_FOOTER) {
+    store_le32(dst + c * dst_stride + nbytes, f);
+    if (out) out[c] = f;
+  } else {
+    out[2 * c] = f;
+    out[2 * c + 1] = load_le32(src + c * src_stride + nbytes);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fused Shuffle(es) + Fletcher32 over batches of chunks, one tile per block
+// (register layout of mc_shuffle.hip).  Needs count % TE == 0.
+// ---------------------------------------------------------------------------
+// weight of the dword at plane byte offset b*count + e (e even): word index
+// j = (b*count + e)/2; c = (nwords - j) mod M
+MC_DEV uint32_t plane_weight(uint32_t cb0, uint32_t cnt_m, int b, uint32_t extra) {
+  // cb0 = (nwords - e0/2) mod M; cnt_m = (count/2) mod M; extra < 2^20
+  const uint32_t x = cb0 + 32u * M - (uint32_t)b * cnt_m - extra;  // > 0 for b < 32
+  return x % M;
+}
+
+template <int ES, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_f32_enc(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    uint32_t *__restrict__ partials) {
+  using G = Geom<ES, 1>;
+  const int tid = threadIdx.x;
+  const size_t tile = blockIdx.x;
+  const size_t c = tile / m.tiles_per_chunk;
+  const size_t t = tile - c * m.tiles_per_chunk;
+  const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TB;
+  uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TE;
+  const uint64_t nwords = (uint64_t)m.count * ES / 2;
+  const size_t e0 = t * (size_t)G::TE + 4 * (size_t)tid;
+  const uint32_t cb0 = (uint32_t)((nwords - e0 / 2) % M);
+  const uint32_t cnt_m = (uint32_t)((m.count / 2) % M);
+  uint32_t w[G::Q][ES];
+#pragma unroll
+  for (int q = 0; q < G::Q; ++q) load_quad<ES, NT>(s + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
+  F32Part p;
+  part_init(p);
+#pragma unroll
+  for (int q = 0; q < G::Q; ++q) {
+    uint32_t pl[ES];
+    mc_quad_to_planes<ES>(w[q], pl);
+#pragma unroll
+    for (int b = 0; b < ES; ++b) {
+      mc_st4<NT>(d + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4, pl[b]);
+      part_dword(p, pl[b], plane_weight(cb0, cnt_m, b, 2u * MC_BLOCK * q));
+    }
+  }
+  uint32_t s1, s2, nz;
+  block_reduce(p, s1, s2, nz);
+  if (tid == 0) {
+    partials[3 * tile + 0] = s1;
+    partials[3 * tile + 1] = s2;
+    partials[3 * tile + 2] = nz;
+  }
+}
+
+template <int ES, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_f32_unshuffle(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    uint32_t *__restrict__ partials) {
+  using G = Geom<ES, 1>;
+  const int tid = threadIdx.x;
+  const size_t tile = blockIdx.x;
+  const size_t c = tile / m.tiles_per_chunk;
+  const size_t t = tile - c * m.tiles_per_chunk;
+  const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TE;
+  uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TB;
+  const uint64_t nwords = (uint64_t)m.count * ES / 2;
+  const size_t e0 = t * (size_t)G::TE + 4 * (size_t)tid;
+  const uint32_t cb0 = (uint32_t)((nwords - e0 / 2) % M);
+  const uint32_t cnt_m = (uint32_t)((m.count / 2) % M);
+  uint32_t p[G::Q][ES];
+#pragma unroll
+  for (int b = 0; b < ES; ++b)
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q)
+      p[q][b] = mc_ld4<NT>(s + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4);
+  F32Part acc;
+  part_init(acc);
+#pragma unroll
+  for (int q = 0; q < G::Q; ++q) {
+#pragma unroll
+    for (int b = 0; b < ES; ++b) part_dword(acc, p[q][b], plane_weight(cb0, cnt_m, b, 2u * MC_BLOCK * q));
+    uint32_t w[ES];
+    mc_planes_to_quad<ES>(p[q], w);
+    store_quad<ES, NT>(d + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w);
+  }
+  uint32_t s1, s2, nz;
+  block_reduce(acc, s1, s2, nz);
+  if (tid == 0) {
+    partials[3 * tile + 0] = s1;
+    partials[3 * tile + 1] = s2;
+    partials[3 * tile + 2] = nz;
+  }
+}
+
+// slices per chunk for the standalone checksum: ~64 KiB of payload per block,
+// at least one block per chunk
+static unsigned slices_for(size_t nbytes, size_t nchunks) {
+  size_t sl = nbytes / (64 * 1024);
+  if (sl < 1) sl = 1;
+  if (sl > 65536) sl = 65536;
+  // keep the grid within a 32-bit block count
+  while (sl > 1 && sl * nchunks > 0x7fffffffull) sl >>= 1;
+  (void)nchunks;
+  return (unsigned)sl;
+}
+
+static size_t partials_bytes(size_t nchunks, unsigned nslices) {
+  return nchunks * (size_t)nslices * 3 * sizeof(uint32_t);
+}
+
+// standalone driver: checksum (+ optional copy) of nchunks chunks, then finalize
+static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
+                   size_t nchunks, size_t nbytes, int mode, uint32_t *out, void *ws,
+                   size_t ws_bytes, hipStream_t st) {
+  const unsigned nsl = slices_for(nbytes, nchunks);
+  if (!ws || ws_bytes < partials_bytes(nchunks, nsl)) return MC_ENOSPC;
+  uint32_t *partials = static_cast<uint32_t *>(ws);
+  const bool copy = dst != nullptr && mode != F_VERIFY;
+  const bool vec = ((uintptr_t)src % 16 == 0) && (src_stride % 16 == 0 || nchunks == 1) &&
+                   (!copy || (((uintptr_t)dst % 16 == 0) && (dst_stride % 16 == 0 || nchunks == 1)));
+  const size_t grid = nchunks * nsl;
+  if (copy) {
+    if (vec) k_f32_partial<true, true><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, partials);
+    else k_f32_partial<true, false><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, partials);
+  } else {
+    if (vec) k_f32_partial<false, true><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, nullptr, 0, nbytes, nsl, partials);
+    else k_f32_partial<false, false><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, nullptr, 0, nbytes, nsl, partials);
+  }
+  int rc = mc_last_launch();
+  if (rc != MC_OK) return rc;
+  const unsigned fgrid = (unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK);
+  k_f32_finalize<<<fgrid, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride, dst,
+                                             dst_stride, nbytes, out);
+  return mc_last_launch();
+}
+
+static size_t fused_tile_elems(size_t es) { return es >= 16 ? 2048 : 4096; }
+
+static bool fused_ok(const void *src, size_t src_stride, const void *dst, size_t dst_stride,
+                     size_t nchunks, size_t chunk_bytes, size_t es) {
+  if (!(es == 2 || es == 4 || es == 8 || es == 16)) return false;
+  if (chunk_bytes % es != 0) return false;
+  const size_t count = chunk_bytes / es;
+  if (count % fused_tile_elems(es) != 0) return false;
+  if ((uintptr_t)src % 16 || (uintptr_t)dst % 16) return false;
+  if (nchunks > 1 && (src_stride % 16 || dst_stride % 16)) return false;
+  return true;
+}
+
+}  // namespace
+
+// shared with mc_shuffle.hip
+int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_stride,
+                    size_t nchunks, size_t chunk_bytes, size_t es, bool enc, int variant,
+                    int max_blocks, const McBitRound *br, hipStream_t st);
+
+extern "C" {
+
+size_t mc_fletcher32_workspace(size_t nbytes) {
+  return partials_bytes(1, slices_for(nbytes, 1));
+}
+
+int mc_fletcher32(const void *src, size_t nbytes, uint32_t *out_sum, void *workspace,
+                  size_t workspace_bytes, mc_stream_t stream) {
+  if (!out_sum || (!src && nbytes)) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (nbytes == 0) return mc_hip_status(hipMemsetAsync(out_sum, 0, sizeof(uint32_t), st));
+  return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, nbytes, F_SUM, out_sum,
+                 workspace, workspace_bytes, st);
+}
+
+int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes, void *workspace,
+                         size_t workspace_bytes, mc_stream_t stream) {
+  if (!src || !dst || nbytes == 0) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), 0, static_cast<uint8_t *>(dst), 0, 1, nbytes,
+                 F_FOOTER, nullptr, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair, void *workspace,
+                         size_t workspace_bytes, mc_stream_t stream) {
+  if (!src || !out_pair || nbytes < 4) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t payload = nbytes - 4;  // payload 0: checksum 0, footer still read
+  return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, payload, F_VERIFY, out_pair,
+                 workspace, workspace_bytes, st);
+}
+
+int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks, size_t chunk_bytes,
+                        uint32_t *out_sums, void *workspace, size_t workspace_bytes,
+                        mc_stream_t stream) {
+  if (nchunks == 0) return MC_OK;
+  if (!src || !out_sums || (nchunks > 1 && stride < chunk_bytes)) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (chunk_bytes == 0) return mc_hip_status(hipMemsetAsync(out_sums, 0, nchunks * 4, st));
+  return f32_run(static_cast<const uint8_t *>(src), stride, nullptr, 0, nchunks, chunk_bytes, F_SUM,
+                 out_sums, workspace, workspace_bytes, st);
+}
+
+size_t mc_fletcher32_batch_workspace(size_t nchunks, size_t chunk_bytes) {
+  return partials_bytes(nchunks, slices_for(chunk_bytes, nchunks));
+}
+
+size_t mc_shuffle_fletcher32_workspace(size_t nchunks, size_t chunk_bytes, size_t elementsize) {
+  // fused path: one partial per tile; fallback path: the standalone slices
+  const size_t es = elementsize ? elementsize : 1;
+  const size_t tiles = (es == 2 || es == 4 || es == 8 || es == 16) && chunk_bytes % es == 0
+                           ? (chunk_bytes / es) / fused_tile_elems(es) + 1
+                           : 1;
+  const size_t a = nchunks * tiles * 3 * sizeof(uint32_t);
+  const size_t b = partials_bytes(nchunks, slices_for(chunk_bytes, nchunks));
+  return a > b ? a : b;
+}
+
+int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void *dst,
+                                       size_t dst_stride, size_t nchunks, size_t chunk_bytes,
+                                       size_t elementsize, void *workspace,
+                                       size_t workspace_bytes, mc_stream_t stream) {
+  if (nchunks == 0) return MC_OK;
+  if (!src || !dst || chunk_bytes == 0) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < chunk_bytes || dst_stride < chunk_bytes + 4)) return MC_EINVAL;
+  if (workspace_bytes < mc_shuffle_fletcher32_workspace(nchunks, chunk_bytes, elementsize) || !workspace)
+    return MC_ENOSPC;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const size_t es = elementsize ? elementsize : 1;
+  if (nchunks == 1) { src_stride = chunk_bytes; dst_stride = chunk_bytes + 4; }
+  if (!fused_ok(src, src_stride, dst, dst_stride, nchunks, chunk_bytes, es)) {
+    // two passes: shuffle into place, then checksum + footer over the result
+    int rc = mc_shuffle_impl(src, src_stride, dst, dst_stride, nchunks, chunk_bytes, es, true, 0, 0,
+                             nullptr, st);
+    if (rc != MC_OK) return rc;
+    const unsigned nsl = slices_for(chunk_bytes, nchunks);
+    uint32_t *partials = static_cast<uint32_t *>(workspace);
+    const bool vec = ((uintptr_t)d % 16 == 0) && (dst_stride % 16 == 0);
+    if (vec) k_f32_partial<false, true><<<(unsigned)(nchunks * nsl), MC_BLOCK, 0, st>>>(d, dst_stride, nullptr, 0, chunk_bytes, nsl, partials);
+    else k_f32_partial<false, false><<<(unsigned)(nchunks * nsl), MC_BLOCK, 0, st>>>(d, dst_stride, nullptr, 0, chunk_bytes, nsl, partials);
+    rc = mc_last_launch();
+    if (rc != MC_OK) return rc;
+    k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+        partials, nsl, nchunks, F_FOOTER, nullptr, 0, d, dst_stride, chunk_bytes, nullptr);
+    return mc_last_launch();
+  }
+  ChunkMap m;
+  m.count = chunk_bytes / es;
+  m.tiles_per_chunk = m.count / fused_tile_elems(es);
+  m.src_stride = src_stride;
+  m.dst_stride = dst_stride;
+  m.group = 1;
+  const size_t ntiles = m.tiles_per_chunk * nchunks;
+  uint32_t *partials = static_cast<uint32_t *>(workspace);
+  switch (es) {
+    case 2: k_shuffle_f32_enc<2, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    case 4: k_shuffle_f32_enc<4, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    case 8: k_shuffle_f32_enc<8, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    default: k_shuffle_f32_enc<16, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+  }
+  int rc = mc_last_launch();
+  if (rc != MC_OK) return rc;
+  k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+      partials, (unsigned)m.tiles_per_chunk, nchunks, F_FOOTER, nullptr, 0, d, dst_stride,
+      chunk_bytes, nullptr);
+  return mc_last_launch();
+}
+
+int mc_fletcher32_unshuffle_batch(const void *src, size_t src_stride, void *dst,
+                                  size_t dst_stride, size_t nchunks, size_t chunk_bytes,
+                                  size_t elementsize, uint32_t *status, void *workspace,
+                                  size_t workspace_bytes, mc_stream_t stream) {
+  if (nchunks == 0) return MC_OK;
+  if (!src || !dst || !status || chunk_bytes == 0) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < chunk_bytes + 4 || dst_stride < chunk_bytes)) return MC_EINVAL;
+  if (workspace_bytes < mc_shuffle_fletcher32_workspace(nchunks, chunk_bytes, elementsize) || !workspace)
+    return MC_ENOSPC;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const size_t es = elementsize ? elementsize : 1;
+  if (nchunks == 1) { src_stride = chunk_bytes + 4; dst_stride = chunk_bytes; }
+  if (!fused_ok(src, src_stride, dst, dst_stride, nchunks, chunk_bytes, es)) {
+    // two passes: verify over the payloads, then unshuffle
+    int rc = f32_run(s, src_stride, nullptr, 0, nchunks, chunk_bytes, F_VERIFY, status, workspace,
+                     workspace_bytes, st);
+    if (rc != MC_OK) return rc;
+    return mc_shuffle_impl(src, src_stride, dst, dst_stride, nchunks, chunk_bytes, es, false, 0, 0,
+                           nullptr, st);
+  }
+  ChunkMap m;
+  m.count = chunk_bytes / es;
+  m.tiles_per_chunk = m.count / fused_tile_elems(es);
+  m.src_stride = src_stride;
+  m.dst_stride = dst_stride;
+  m.group = 1;
+  const size_t ntiles = m.tiles_per_chunk * nchunks;
+  uint32_t *partials = static_cast<uint32_t *>(workspace);
+  switch (es) {
+    case 2: k_f32_unshuffle<2, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    case 4: k_f32_unshuffle<4, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    case 8: k_f32_unshuffle<8, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+    default: k_f32_unshuffle<16, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, m, partials); break;
+  }
+  int rc = mc_last_launch();
+  if (rc != MC_OK) return rc;
+  k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+      partials, (unsigned)m.tiles_per_chunk, nchunks, F_VERIFY, s, src_stride, nullptr, 0,
+      chunk_bytes, status);
+  return mc_last_launch();
+}
+
+}  // extern "C"

@@ -1,0 +1,569 @@
+// mc_shuffle.hip -- Shuffle (byte transpose) encode/decode for gfx950.
+//
+// Reference: src/numcodecs/_shuffle.pyx:11-18 (_doShuffle) and :23-30
+// (_doUnshuffle), driven by shuffle.py:40-58.  With count = nbytes / es:
+//   encode: dst[b*count + i] = src[i*es + b]
+//   decode: dst[i*es + b]    = src[b*count + i]
+//
+// Design (HBM-bound byte work, no MFMA):
+//   * A tile is TE consecutive elements (TE = 4096 for es <= 8, 2048 for
+//     es = 16): es*TE bytes on the element side, es planes of TE bytes on the
+//     plane side.  One 256-thread workgroup moves one tile per iteration of a
+//     grid-stride loop; each thread owns Q "quads" of 4 consecutive elements.
+//   * A quad's es dwords are turned into its es plane dwords by a 4x4 byte
+//     transpose in registers (v_perm_b32, mc_tr4), so every lane always moves
+//     whole dwords.
+//   * The element side is read/written with 16-B (es = 4, 8, 16) or 8-B
+//     (es = 2) accesses per lane; the plane side either directly with one
+//     dword per lane per plane (256 contiguous bytes per wave instruction) or
+//     staged through LDS so that it too moves 16 B per lane (1 KiB per wave
+//     instruction).  Which combination is fastest is measured (bench.py
+//     --sweep) and the winner per (es, direction) is the default.
+//   * Sizes that are not a whole number of tiles finish with a generic
+//     byte-granular kernel over the tail elements; unaligned buffers or
+//     count % 4 != 0 run entirely on the generic kernel.
+#include "mc_shuffle.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// encode tile kernel
+// ---------------------------------------------------------------------------
+template <int ES, bool BITROUND, bool IN_LDS, bool OUT_LDS, bool NT, int QMUL = 1>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_enc(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t ntiles, McBitRound br) {
+  using G = Geom<ES, QMUL>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TE;
+
+    uint32_t p[G::Q][ES];
+    if constexpr (IN_LDS) {
+      mc_u32x4 v[G::NV];
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r)
+        v[r] = mc_ld16<NT>(s + (size_t)(r * MC_BLOCK + tid) * 16);
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r)
+        reinterpret_cast<mc_u32x4 *>(lds)[r * MC_BLOCK + tid] = v[r];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q) {
+        uint32_t w[ES];
+        load_quad<ES, false>(lds + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w);
+        if constexpr (BITROUND) mc_bitround_quad<ES>(w, br);
+        mc_quad_to_planes<ES>(w, p[q]);
+      }
+      __syncthreads();
+    } else {
+      uint32_t w[G::Q][ES];
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+        load_quad<ES, NT>(s + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q) {
+        if constexpr (BITROUND) mc_bitround_quad<ES>(w[q], br);
+        mc_quad_to_planes<ES>(w[q], p[q]);
+      }
+    }
+
+    if constexpr (OUT_LDS) {
+      // plane-major image: plane b, quad qi -> dword b*(TE/4) + qi
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+#pragma unroll
+        for (int b = 0; b < ES; ++b)
+          reinterpret_cast<uint32_t *>(lds)[b * (G::TE / 4) + q * MC_BLOCK + tid] = p[q][b];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r) {
+        const int u = r * MC_BLOCK + tid;
+        const int b = u / G::PU;
+        const int j = u - b * G::PU;
+        const mc_u32x4 v = reinterpret_cast<const mc_u32x4 *>(lds)[u];
+        mc_st16<NT>(d + (size_t)b * m.count + (size_t)j * 16, v);
+      }
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int b = 0; b < ES; ++b)
+#pragma unroll
+        for (int q = 0; q < G::Q; ++q)
+          mc_st4<NT>(d + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4, p[q][b]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// decode tile kernel
+// ---------------------------------------------------------------------------
+template <int ES, bool IN_LDS, bool OUT_LDS, bool NT, int QMUL = 1>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t ntiles) {
+  using G = Geom<ES, QMUL>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TE;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TB;
+
+    uint32_t w[G::Q][ES];
+    if constexpr (IN_LDS) {
+      mc_u32x4 v[G::NV];
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r) {
+        const int u = r * MC_BLOCK + tid;
+        const int b = u / G::PU;
+        const int j = u - b * G::PU;
+        v[r] = mc_ld16<NT>(s + (size_t)b * m.count + (size_t)j * 16);
+      }
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r)
+        reinterpret_cast<mc_u32x4 *>(lds)[r * MC_BLOCK + tid] = v[r];
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q) {
+        uint32_t p[ES];
+#pragma unroll
+        for (int b = 0; b < ES; ++b)
+          p[b] = reinterpret_cast<const uint32_t *>(lds)[b * (G::TE / 4) + q * MC_BLOCK + tid];
+        mc_planes_to_quad<ES>(p, w[q]);
+      }
+      __syncthreads();
+    } else {
+      uint32_t p[G::Q][ES];
+#pragma unroll
+      for (int b = 0; b < ES; ++b)
+#pragma unroll
+        for (int q = 0; q < G::Q; ++q)
+          p[q][b] = mc_ld4<NT>(s + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4);
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q) mc_planes_to_quad<ES>(p[q], w[q]);
+    }
+
+    if constexpr (OUT_LDS) {
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+        store_quad<ES, false>(lds + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < G::NV; ++r)
+        mc_st16<NT>(d + (size_t)(r * MC_BLOCK + tid) * 16,
+                    reinterpret_cast<const mc_u32x4 *>(lds)[r * MC_BLOCK + tid]);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+        store_quad<ES, NT>(d + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// software-pipelined persistent variants (register layout): the next tile's
+// loads are issued before this tile's stores, so waiting for them does not
+// wait for the stores (vmcnt retires loads and stores in issue order).
+// ---------------------------------------------------------------------------
+template <int ES, bool BITROUND, bool NT, int QMUL>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_enc_pipe(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t ntiles, McBitRound br) {
+  using G = Geom<ES, QMUL>;
+  const int tid = threadIdx.x;
+  size_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  auto src_of = [&](size_t tl) {
+    const size_t c = tl / m.tiles_per_chunk;
+    return src + c * m.src_stride + (tl - c * m.tiles_per_chunk) * (size_t)G::TB;
+  };
+  uint32_t w[G::Q][ES];
+  {
+    const uint8_t *s = src_of(tile);
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q)
+      load_quad<ES, NT>(s + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
+  }
+  for (;;) {
+    const size_t nxt = tile + gridDim.x;
+    uint32_t wn[G::Q][ES];
+    if (nxt < ntiles) {
+      const uint8_t *s = src_of(nxt);
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+        load_quad<ES, NT>(s + (size_t)(q * MC_BLOCK + tid) * 4 * ES, wn[q]);
+    }
+    const size_t c = tile / m.tiles_per_chunk;
+    uint8_t *d = dst + c * m.dst_stride + (tile - c * m.tiles_per_chunk) * (size_t)G::TE;
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      uint32_t pl[ES];
+      if constexpr (BITROUND) mc_bitround_quad<ES>(w[q], br);
+      mc_quad_to_planes<ES>(w[q], pl);
+#pragma unroll
+      for (int b = 0; b < ES; ++b)
+        mc_st4<NT>(d + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4, pl[b]);
+    }
+    if (nxt >= ntiles) break;
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q)
+#pragma unroll
+      for (int k = 0; k < ES; ++k) w[q][k] = wn[q][k];
+    tile = nxt;
+  }
+}
+
+template <int ES, bool NT, int QMUL>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec_pipe(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t ntiles) {
+  using G = Geom<ES, QMUL>;
+  const int tid = threadIdx.x;
+  size_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  auto src_of = [&](size_t tl) {
+    const size_t c = tl / m.tiles_per_chunk;
+    return src + c * m.src_stride + (tl - c * m.tiles_per_chunk) * (size_t)G::TE;
+  };
+  uint32_t p[G::Q][ES];
+  {
+    const uint8_t *s = src_of(tile);
+#pragma unroll
+    for (int b = 0; b < ES; ++b)
+#pragma unroll
+      for (int q = 0; q < G::Q; ++q)
+        p[q][b] = mc_ld4<NT>(s + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4);
+  }
+  for (;;) {
+    const size_t nxt = tile + gridDim.x;
+    uint32_t pn[G::Q][ES];
+    if (nxt < ntiles) {
+      const uint8_t *s = src_of(nxt);
+#pragma unroll
+      for (int b = 0; b < ES; ++b)
+#pragma unroll
+        for (int q = 0; q < G::Q; ++q)
+          pn[q][b] = mc_ld4<NT>(s + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4);
+    }
+    const size_t c = tile / m.tiles_per_chunk;
+    uint8_t *d = dst + c * m.dst_stride + (tile - c * m.tiles_per_chunk) * (size_t)G::TB;
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      uint32_t w[ES];
+      mc_planes_to_quad<ES>(p[q], w);
+      store_quad<ES, NT>(d + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w);
+    }
+    if (nxt >= ntiles) break;
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q)
+#pragma unroll
+      for (int k = 0; k < ES; ++k) p[q][k] = pn[q][k];
+    tile = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generic byte-granular kernels (any es >= 2, any count, any alignment):
+// elements [e_begin, count) of every chunk.
+// ---------------------------------------------------------------------------
+template <bool BITROUND>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_enc_generic(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t es, size_t e_begin, size_t nchunks, McBitRound br) {
+  const size_t span = m.count - e_begin;
+  const size_t total = span * nchunks;
+  for (size_t idx = (size_t)blockIdx.x * MC_BLOCK + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * MC_BLOCK) {
+    const size_t c = idx / span;
+    const size_t i = e_begin + (idx - c * span);
+    const uint8_t *s = src + c * m.src_stride + i * es;
+    uint8_t *d = dst + c * m.dst_stride + i;
+    if constexpr (BITROUND) {
+      uint64_t v = 0;
+      for (size_t b = 0; b < es; ++b) v |= (uint64_t)s[b] << (8 * b);
+      if (es == 2) v = mc_bitround16x2((uint32_t)v, br) & 0xffffu;
+      else if (es == 4) v = mc_bitround32((uint32_t)v, br);
+      else v = mc_bitround64(v, br);
+      for (size_t b = 0; b < es; ++b) d[b * m.count] = (uint8_t)(v >> (8 * b));
+    } else {
+      for (size_t b = 0; b < es; ++b) d[b * m.count] = s[b];
+    }
+  }
+}
+
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec_generic(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m,
+    size_t es, size_t e_begin, size_t nchunks) {
+  const size_t span = m.count - e_begin;
+  const size_t total = span * nchunks;
+  for (size_t idx = (size_t)blockIdx.x * MC_BLOCK + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * MC_BLOCK) {
+    const size_t c = idx / span;
+    const size_t i = e_begin + (idx - c * span);
+    const uint8_t *s = src + c * m.src_stride + i;
+    uint8_t *d = dst + c * m.dst_stride + i * es;
+    for (size_t b = 0; b < es; ++b) d[b] = s[b * m.count];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4 };
+// variant | V_NO_NT selects default-policy (temporal) global accesses
+static constexpr int V_NO_NT = 8;
+// variant | V_BIG selects 2x larger tiles, | V_BIG4 4x (register layout only)
+static constexpr int V_BIG = 16;
+static constexpr int V_BIG4 = 128;
+// bits 5-6: log2 of the tile group taken per block step (MC_FOR_TILES)
+static constexpr int V_GROUP_SHIFT = 5;
+static constexpr int V_GROUP_MASK = 3 << V_GROUP_SHIFT;
+// variant | V_PIPE: software-pipelined persistent loop (register layout only)
+static constexpr int V_PIPE = 256;
+
+// Measured defaults (tools/probe_enc.py on MI355X, interleaved rounds; the
+// sweep is summarised in DESIGN.md).  Large buffers: one big tile per
+// workgroup and a grid covering every tile (a looping workgroup waits for its
+// previous tile's stores before it can use the next tile's loads, because
+// vmcnt retires loads and stores in issue order).  Small buffers: 4096-element
+// tiles so that there are enough workgroups.
+static int default_variant(size_t es, bool enc, size_t total_bytes, unsigned *grid_cap) {
+  *grid_cap = 0x7fffffffu;
+  if (total_bytes < ((size_t)64 << 20)) return V_REG;
+  switch (es) {
+    case 2: return V_REG | V_BIG4;                       // 6.34 / 6.22 TB/s
+    case 4: return enc ? (V_REG | V_BIG4) : (V_REG | V_BIG);  // 6.1 / 6.2 TB/s
+    case 8:
+      if (enc) return V_REG | V_BIG4;                    // 5.4 TB/s
+      *grid_cap = MC_MAX_GRID;
+      return V_BOTH_LDS;                                 // 5.5 TB/s
+    default:
+      if (enc) return V_REG | V_BIG;
+      *grid_cap = MC_MAX_GRID;
+      return V_BOTH_LDS;
+  }
+}
+
+template <int ES, bool BR, bool NT>
+static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
+                          size_t ntiles, unsigned grid, const McBitRound &br, hipStream_t st) {
+  using G = Geom<ES>;
+  if (layout == (V_REG | V_PIPE | V_BIG4))
+    k_shuffle_enc_pipe<ES, BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == (V_REG | V_PIPE | V_BIG))
+    k_shuffle_enc_pipe<ES, BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == (V_REG | V_PIPE))
+    k_shuffle_enc_pipe<ES, BR, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == (V_REG | V_BIG4))
+    k_shuffle_enc<ES, BR, false, false, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == (V_REG | V_BIG))
+    k_shuffle_enc<ES, BR, false, false, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == V_REG)
+    k_shuffle_enc<ES, BR, false, false, NT><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == V_PLANE_LDS)
+    k_shuffle_enc<ES, BR, false, true, NT><<<grid, MC_BLOCK, G::TB, st>>>(s, d, m, ntiles, br);
+  else
+    k_shuffle_enc<ES, BR, true, true, NT><<<grid, MC_BLOCK, G::TB, st>>>(s, d, m, ntiles, br);
+}
+
+template <int ES, bool BR>
+static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
+                            size_t ntiles, unsigned grid, const McBitRound &br,
+                            hipStream_t st) {
+  const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
+  if ((layout & 7) < V_REG || (layout & 7) > V_BOTH_LDS) return MC_EINVAL;
+  if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
+  else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
+  return mc_last_launch();
+}
+
+template <int ES, bool NT>
+static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
+                          size_t ntiles, unsigned grid, hipStream_t st) {
+  using G = Geom<ES>;
+  if (layout == (V_REG | V_PIPE | V_BIG4))
+    k_shuffle_dec_pipe<ES, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == (V_REG | V_PIPE | V_BIG))
+    k_shuffle_dec_pipe<ES, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == (V_REG | V_PIPE))
+    k_shuffle_dec_pipe<ES, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == (V_REG | V_BIG4))
+    k_shuffle_dec<ES, false, false, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == (V_REG | V_BIG))
+    k_shuffle_dec<ES, false, false, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == V_REG)
+    k_shuffle_dec<ES, false, false, NT><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == V_PLANE_LDS)
+    k_shuffle_dec<ES, true, false, NT><<<grid, MC_BLOCK, G::TB, st>>>(s, d, m, ntiles);
+  else
+    k_shuffle_dec<ES, true, true, NT><<<grid, MC_BLOCK, G::TB, st>>>(s, d, m, ntiles);
+}
+
+template <int ES>
+static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
+                            size_t ntiles, unsigned grid, hipStream_t st) {
+  const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
+  if ((layout & 7) < V_REG || (layout & 7) > V_BOTH_LDS) return MC_EINVAL;
+  if (variant & V_NO_NT) launch_dec_nt<ES, false>(layout, s, d, m, ntiles, grid, st);
+  else launch_dec_nt<ES, true>(layout, s, d, m, ntiles, grid, st);
+  return mc_last_launch();
+}
+
+static size_t tile_elems(size_t es, int variant) {
+  const size_t te = es >= 16 ? 2048 : 4096;
+  if ((variant & 7) != V_REG) return te;
+  return (variant & V_BIG4) ? 4 * te : (variant & V_BIG) ? 2 * te : te;
+}
+
+}  // namespace
+
+// Shared driver for every shuffle entry point (also used by the fused ops).
+int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_stride,
+                    size_t nchunks, size_t chunk_bytes, size_t es, bool enc,
+                    int variant, int max_blocks, const McBitRound *br,
+                    hipStream_t st) {
+  if (nchunks == 0 || chunk_bytes == 0) return MC_OK;
+  if (!src_ || !dst_) return MC_EINVAL;
+  const uint8_t *src = static_cast<const uint8_t *>(src_);
+  uint8_t *dst = static_cast<uint8_t *>(dst_);
+  if (es == 0) es = 1;
+  if (chunk_bytes % es != 0) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < chunk_bytes || dst_stride < chunk_bytes)) return MC_EINVAL;
+
+  if (es == 1 && br == nullptr) {  // "no shuffling needed" (shuffle.py:31-33)
+    if (nchunks == 1)
+      return mc_hip_status(hipMemcpyAsync(dst, src, chunk_bytes, hipMemcpyDeviceToDevice, st));
+    return mc_hip_status(hipMemcpy2DAsync(dst, dst_stride, src, src_stride, chunk_bytes,
+                                          nchunks, hipMemcpyDeviceToDevice, st));
+  }
+
+  ChunkMap m;
+  m.count = chunk_bytes / es;
+  m.src_stride = nchunks > 1 ? src_stride : 0;
+  m.dst_stride = nchunks > 1 ? dst_stride : 0;
+  m.group = 1;
+
+  unsigned default_cap = MC_MAX_GRID;
+  if (variant == V_DEFAULT) {
+    variant = default_variant(es, enc, chunk_bytes * nchunks, &default_cap);
+    if (max_blocks <= 0) max_blocks = (int)default_cap;
+  }
+  const bool fast_es = es == 2 || es == 4 || es == 8 || es == 16;
+  const bool aligned16 = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0) &&
+                         (m.src_stride % 16 == 0) && (m.dst_stride % 16 == 0);
+  if (!fast_es || !aligned16 || m.count % 4 != 0 || (br && es == 16)) variant = V_GENERIC;
+  // the 16-B plane-side accesses need 16-B aligned plane bases
+  if ((variant & 7) != V_GENERIC && (variant & 7) != V_REG && m.count % 16 != 0)
+    variant = V_REG | (variant & (V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE));
+
+  size_t e_done = 0;
+  McBitRound nobr{};
+  const McBitRound &brr = br ? *br : nobr;
+  if ((variant & 7) != V_GENERIC) {
+    if ((variant & 7) != V_REG) variant &= ~(V_BIG | V_BIG4 | V_PIPE);
+    if (variant & V_PIPE) variant &= ~V_GROUP_MASK;
+    if (variant & V_BIG4) variant &= ~V_BIG;
+    m.group = 1u << ((variant & V_GROUP_MASK) >> V_GROUP_SHIFT);
+    const size_t te = tile_elems(es, variant);
+    m.tiles_per_chunk = m.count / te;
+    const size_t ntiles = m.tiles_per_chunk * nchunks;
+    if (ntiles > 0) {
+      unsigned cap = max_blocks > 0 ? (unsigned)max_blocks : MC_MAX_GRID;
+      unsigned grid = mc_grid_for(ntiles, m.group, cap);
+      int rc = MC_EINVAL;
+      if (enc) {
+        switch (es) {
+          case 2: rc = br ? launch_enc_tiles<2, true>(variant, src, dst, m, ntiles, grid, brr, st)
+                          : launch_enc_tiles<2, false>(variant, src, dst, m, ntiles, grid, brr, st); break;
+          case 4: rc = br ? launch_enc_tiles<4, true>(variant, src, dst, m, ntiles, grid, brr, st)
+                          : launch_enc_tiles<4, false>(variant, src, dst, m, ntiles, grid, brr, st); break;
+          case 8: rc = br ? launch_enc_tiles<8, true>(variant, src, dst, m, ntiles, grid, brr, st)
+                          : launch_enc_tiles<8, false>(variant, src, dst, m, ntiles, grid, brr, st); break;
+          case 16: rc = launch_enc_tiles<16, false>(variant, src, dst, m, ntiles, grid, brr, st); break;
+        }
+      } else {
+        switch (es) {
+          case 2: rc = launch_dec_tiles<2>(variant, src, dst, m, ntiles, grid, st); break;
+          case 4: rc = launch_dec_tiles<4>(variant, src, dst, m, ntiles, grid, st); break;
+          case 8: rc = launch_dec_tiles<8>(variant, src, dst, m, ntiles, grid, st); break;
+          case 16: rc = launch_dec_tiles<16>(variant, src, dst, m, ntiles, grid, st); break;
+        }
+      }
+      if (rc != MC_OK) return rc;
+    }
+    e_done = m.tiles_per_chunk * te;
+  }
+  if (e_done < m.count) {
+    m.tiles_per_chunk = 0;
+    const size_t total = (m.count - e_done) * nchunks;
+    const unsigned grid = mc_grid_for(total, MC_BLOCK);
+    if (enc) {
+      if (br) k_shuffle_enc_generic<true><<<grid, MC_BLOCK, 0, st>>>(src, dst, m, es, e_done, nchunks, brr);
+      else k_shuffle_enc_generic<false><<<grid, MC_BLOCK, 0, st>>>(src, dst, m, es, e_done, nchunks, brr);
+    } else {
+      k_shuffle_dec_generic<<<grid, MC_BLOCK, 0, st>>>(src, dst, m, es, e_done, nchunks);
+    }
+    return mc_last_launch();
+  }
+  return MC_OK;
+}
+
+extern "C" {
+
+int mc_shuffle(const void *src, void *dst, size_t nbytes, size_t elementsize,
+               mc_stream_t stream) {
+  return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, true, V_DEFAULT, 0,
+                         nullptr, (hipStream_t)stream);
+}
+
+int mc_unshuffle(const void *src, void *dst, size_t nbytes, size_t elementsize,
+                 mc_stream_t stream) {
+  return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, false, V_DEFAULT, 0,
+                         nullptr, (hipStream_t)stream);
+}
+
+int mc_shuffle_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                     size_t nchunks, size_t chunk_bytes, size_t elementsize,
+                     mc_stream_t stream) {
+  return mc_shuffle_impl(src, src_stride, dst, dst_stride, nchunks, chunk_bytes,
+                         elementsize, true, V_DEFAULT, 0, nullptr, (hipStream_t)stream);
+}
+
+int mc_unshuffle_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                       size_t nchunks, size_t chunk_bytes, size_t elementsize,
+                       mc_stream_t stream) {
+  return mc_shuffle_impl(src, src_stride, dst, dst_stride, nchunks, chunk_bytes,
+                         elementsize, false, V_DEFAULT, 0, nullptr, (hipStream_t)stream);
+}
+
+int mc_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize,
+                       int encode, int variant, int max_blocks, mc_stream_t stream) {
+  if (variant < 0 || (variant & 7) > V_GENERIC ||
+      (variant & ~(7 | V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE)) != 0)
+    return MC_EINVAL;
+  return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant,
+                         max_blocks, nullptr, (hipStream_t)stream);
+}
+
+int mc_bitround_shuffle(const void *src, void *dst, size_t n, int itemsize, int keepbits,
+                        mc_stream_t stream) {
+  if (!(itemsize == 2 || itemsize == 4 || itemsize == 8)) return MC_EINVAL;
+  const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
+  if (keepbits < 0 || keepbits > mbits) return MC_EINVAL;
+  if (keepbits == mbits)  // identity rounding: plain shuffle
+    return mc_shuffle(src, dst, n * (size_t)itemsize, (size_t)itemsize, stream);
+  const McBitRound br = mc_make_bitround(itemsize, keepbits);
+  return mc_shuffle_impl(src, 0, dst, 0, 1, n * (size_t)itemsize, (size_t)itemsize, true,
+                         V_DEFAULT, 0, &br, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+"""Delta codec (reference: src/numcodecs/delta.py:7-94).
+
+encode: first element, then adjacent differences computed in `dtype` and
+cast to `astype` (one fused pass, csrc/mc_elementwise.hip: k_delta_enc).
+decode: running sum accumulated in `dtype` (csrc/mc_scan.hip): a parallel
+scan for integer/bool dtypes (wrap-around arithmetic, bit-exact), and
+numpy's exact left-to-right order for float dtypes.
+"""
+
+import numpy as np
+
+from . import _ops
+from .abc import Codec
+from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
+
+__all__ = ["Delta"]
+
+
+class Delta(Codec):
+    """Codec to encode data as the difference between adjacent values.
+
+    Parameters
+    ----------
+    dtype : dtype
+        Data type to use for decoded data.
+    astype : dtype, optional
+        Data type to use for encoded data.
+
+    Notes
+    -----
+    If `astype` is an integer data type, please ensure that it is
+    sufficiently large to store encoded values. No checks are made and data
+    may become corrupted due to integer overflow if `astype` is too small.
+
+    Examples
+    --------
+    >>> import numpy as np
+    >>> import numcodecs_amd
+    >>> x = np.arange(100, 120, 2, dtype='i2')
+    >>> codec = numcodecs_amd.Delta(dtype='i2', astype='i1')
+    >>> codec.encode(x)  # doctest: +SKIP
+    array([100,   2,   2,   2,   2,   2,   2,   2,   2,   2], dtype=int8)
+    """
+
+    codec_id = "delta"
+
+    def __init__(self, dtype, astype=None):
+        self.dtype = np.dtype(dtype)
+        self.astype = self.dtype if astype is None else np.dtype(astype)
+        if self.dtype == np.dtype(object) or self.astype == np.dtype(object):
+            raise ValueError("object arrays are not supported")
+
+    def encode(self, buf):
+        src = to_dbuf(buf, contiguous=False)
+        if src.nbytes % self.dtype.itemsize:
+            raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
+        n = src.nbytes // self.dtype.itemsize
+        if n == 0:  # enc[0] = arr[0] on an empty array (delta.py:63)
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        dst = empty_like_bytes(n * self.astype.itemsize, src)
+        _ops.delta_encode(src.data, dst, n, self.dtype, self.astype)
+        return finish(dst, self.astype, (n,), "C", src.host)
+
+    def decode(self, buf, out=None):
+        src = to_dbuf(buf, contiguous=False)
+        if src.nbytes % self.astype.itemsize:
+            raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
+        n = src.nbytes // self.astype.itemsize
+        if not np.can_cast(self.astype, self.dtype, casting="same_kind"):
+            # np.cumsum(enc, out=dec) refuses the output cast (delta.py:80)
+            raise TypeError(
+                f"Cannot cast ufunc 'add' output from {self.astype!r} to {self.dtype!r} "
+                "with casting rule 'same_kind'"
+            )
+        dst = empty_like_bytes(n * self.dtype.itemsize, src)
+        _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)
+        return ndarray_copy(finish(dst, self.dtype, (n,), "C", src.host), out)
+
+    def get_config(self):
+        return {"id": self.codec_id, "dtype": self.dtype.str, "astype": self.astype.str}
+
+    def __repr__(self):
+        r = f"{type(self).__name__}(dtype={self.dtype.str!r}"
+        if self.astype != self.dtype:
+            r += f", astype={self.astype.str!r}"
+        return r + ")"

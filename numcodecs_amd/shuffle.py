@@ -1,0 +1,79 @@
+"""Shuffle codec (reference: src/numcodecs/shuffle.py:8-61, _shuffle.pyx:11-30).
+
+Byte transpose of the (count, elementsize) byte matrix of a chunk, run by
+the gfx950 kernels of libmcodec (csrc/mc_shuffle.hip).
+"""
+
+import numpy as np
+import torch
+
+from . import _ops
+from .abc import Codec
+from .compat import (
+    empty_like_bytes,
+    ensure_contiguous_ndarray,
+    finish,
+    is_device_tensor,
+    to_dbuf,
+    upload,
+)
+
+__all__ = ["Shuffle"]
+
+
+class Shuffle(Codec):
+    """Codec providing shuffle
+
+    Parameters
+    ----------
+    elementsize : int
+        Size in bytes of the array elements.  Default = 4
+    """
+
+    codec_id = "shuffle"
+
+    def __init__(self, elementsize=4):
+        self.elementsize = elementsize
+
+    def _run(self, buf, out, encode):
+        src = to_dbuf(buf)  # ensure_contiguous_ndarray semantics (shuffle.py:24)
+        nbytes = src.nbytes
+        es = self.elementsize
+        if es > 1 and nbytes % es != 0:  # shuffle.py:35-36
+            raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+        if out is not None and not is_device_tensor(out):
+            host_out = ensure_contiguous_ndarray(out)
+            if host_out.nbytes < nbytes:
+                raise ValueError("output buffer is too small for the shuffled data")
+            res = empty_like_bytes(nbytes, src)
+        else:
+            host_out = None
+            if out is not None:
+                out_flat = ensure_contiguous_ndarray(out)
+                res = out_flat.view(torch.uint8) if out_flat.numel() else out_flat.new_empty(0, dtype=torch.uint8)
+                if res.numel() < nbytes:
+                    raise ValueError("output buffer is too small for the shuffled data")
+                if res.device != src.data.device:
+                    raise ValueError("out must be on the same device as the input")
+            else:
+                res = empty_like_bytes(nbytes, src)
+        if es <= 1:  # no shuffling needed (shuffle.py:31-33)
+            res[:nbytes].copy_(src.data)
+        else:
+            _ops.shuffle(src.data, res, nbytes, es, encode)
+        if host_out is not None:
+            tmp = finish(res, np.uint8, (nbytes,), "C", True)
+            host_out.view(np.uint8)[:nbytes] = tmp
+            return host_out
+        if out is not None:
+            return ensure_contiguous_ndarray(out)
+        return finish(res, np.uint8, (nbytes,), "C", src.host)
+
+    def encode(self, buf, out=None):
+        return self._run(buf, out, True)
+
+    def decode(self, buf, out=None):
+        return self._run(buf, out, False)
+
+    def __repr__(self):
+        return f"{type(self).__name__}(elementsize={self.elementsize})"

@@ -1,0 +1,230 @@
+"""Numpy + C restatement of the numcodecs hot path -- TEST INFRASTRUCTURE ONLY.
+
+Every function names the reference lines it restates (paths under
+src/numcodecs/ of zarr-developers/numcodecs).  Inputs are host buffers
+(numpy arrays or bytes-like); outputs mirror what the reference returns.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libncoracle.so")
+_lib = None
+
+
+def _c():
+    """Load (building on first use) the C restatement oracle/ncoracle.c."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            subprocess.run(["make", "-s", "-C", _HERE, "_build/libncoracle.so"], check=True)
+        lib = ctypes.CDLL(_LIB_PATH)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.nco_shuffle.argtypes = [vp, vp, sz, sz]
+        lib.nco_unshuffle.argtypes = [vp, vp, sz, sz]
+        lib.nco_shuffle_batch.argtypes = [vp, vp, sz, sz, sz]
+        lib.nco_unshuffle_batch.argtypes = [vp, vp, sz, sz, sz]
+        lib.nco_fletcher32.argtypes = [vp, sz]
+        lib.nco_fletcher32.restype = ctypes.c_uint32
+        _lib = lib
+    return _lib
+
+
+def _bytes_view(buf) -> np.ndarray:
+    """Flat uint8 view of a contiguous buffer (compat.py:120-150 semantics)."""
+    if isinstance(buf, np.ndarray):
+        a = buf
+        if a.dtype.kind in "Mm":
+            a = a.view("i8")
+        if not (a.flags.c_contiguous or a.flags.f_contiguous):
+            raise ValueError("an array with contiguous memory is required")
+        return a.reshape(-1, order="A").view("u1")
+    return np.frombuffer(memoryview(buf), dtype="u1")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# --------------------------------------------------------------------------
+# Shuffle: _shuffle.pyx:11-30, shuffle.py:23-58
+# --------------------------------------------------------------------------
+def shuffle(buf, elementsize: int) -> np.ndarray:
+    """Shuffle(elementsize).encode(buf) -> uint8 array (shuffle.py:40-48)."""
+    src = np.ascontiguousarray(_bytes_view(buf))
+    out = np.zeros(src.nbytes, dtype="u1")
+    if elementsize <= 1:
+        out[:] = src
+        return out
+    if src.nbytes % elementsize != 0:
+        raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+    if src.nbytes:
+        _c().nco_shuffle(_ptr(src), _ptr(out), src.nbytes, elementsize)
+    return out
+
+
+def unshuffle(buf, elementsize: int) -> np.ndarray:
+    """Shuffle(elementsize).decode(buf) -> uint8 array (shuffle.py:50-58)."""
+    src = np.ascontiguousarray(_bytes_view(buf))
+    out = np.zeros(src.nbytes, dtype="u1")
+    if elementsize <= 1:
+        out[:] = src
+        return out
+    if src.nbytes % elementsize != 0:
+        raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+    if src.nbytes:
+        _c().nco_unshuffle(_ptr(src), _ptr(out), src.nbytes, elementsize)
+    return out
+
+
+# --------------------------------------------------------------------------
+# Fletcher32: fletcher32.pyx:24-115, _utils.pxd:11-24
+# --------------------------------------------------------------------------
+def fletcher32(buf) -> int:
+    """_fletcher32 over the raw bytes (fletcher32.pyx:24-57)."""
+    src = np.ascontiguousarray(_bytes_view(buf))
+    if src.nbytes == 0:
+        return 0
+    return int(_c().nco_fletcher32(_ptr(src), src.nbytes))
+
+
+def fletcher32_encode(buf) -> bytes:
+    """payload + LE32 checksum footer (fletcher32.pyx:75-89)."""
+    src = _bytes_view(buf)
+    if src.nbytes == 0:  # the reference indexes b_mv[0] of an empty view
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    return src.tobytes() + int(fletcher32(src)).to_bytes(4, "little")
+
+
+def fletcher32_decode(buf) -> np.ndarray:
+    """Verify the footer and return the payload view (fletcher32.pyx:91-115)."""
+    b = _bytes_view(buf)
+    if b.nbytes <= 4:
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    val = fletcher32(b[:-4])
+    found = int.from_bytes(b[-4:].tobytes(), "little")
+    if val != found:
+        raise RuntimeError(
+            f"The fletcher32 checksum of the data ({val}) did not"
+            f" match the expected checksum ({found}).\n"
+            "This could be a sign that the data has been corrupted."
+        )
+    return b[:-4]
+
+
+# --------------------------------------------------------------------------
+# BitRound: bitround.py:9-80
+# --------------------------------------------------------------------------
+MAX_BITS = {"float16": 10, "float32": 23, "float64": 52}
+
+
+def bitround_encode(a: np.ndarray, keepbits: int):
+    """bitround.py:45-69 -- round the mantissa on the same-width int view."""
+    if not a.dtype.kind == "f" or a.dtype.itemsize > 8:
+        raise TypeError("Only float arrays (16-64bit) can be bit-rounded")
+    bits = MAX_BITS[str(a.dtype)]
+    int_dtype = np.dtype(a.dtype.str.replace("f", "i"))
+    if keepbits == bits:
+        return a
+    if keepbits > bits:
+        raise ValueError("Keepbits too large for given dtype")
+    b = a.copy().view(int_dtype)
+    maskbits = bits - keepbits
+    all_set = np.array(-1, dtype=int_dtype)
+    mask = (all_set >> maskbits) << maskbits
+    b += ((b >> maskbits) & 1) + ((1 << (maskbits - 1)) - 1)
+    b &= mask
+    return b
+
+
+def bitround_decode(enc: np.ndarray) -> np.ndarray:
+    """bitround.py:71-80 -- re-view the integers as floats."""
+    return enc.view(np.dtype(enc.dtype.str.replace("i", "f")))
+
+
+# --------------------------------------------------------------------------
+# Delta: delta.py:52-83
+# --------------------------------------------------------------------------
+def delta_encode(buf, dtype, astype=None) -> np.ndarray:
+    """enc[0] = x[0]; enc[1:] = np.diff(x) (delta.py:52-67)."""
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    arr = np.asarray(buf).view(dtype).reshape(-1, order="A")
+    enc = np.empty_like(arr, dtype=astype)
+    enc[0] = arr[0]
+    enc[1:] = np.diff(arr)
+    return enc
+
+
+def delta_decode(buf, dtype, astype=None) -> np.ndarray:
+    """np.cumsum(enc, out=dec) accumulated in dtype (delta.py:69-83)."""
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    enc = np.asarray(buf).view(astype).reshape(-1, order="A")
+    dec = np.empty_like(enc, dtype=dtype)
+    np.cumsum(enc, out=dec)
+    return dec
+
+
+# --------------------------------------------------------------------------
+# Quantize: quantize.py:60-82
+# --------------------------------------------------------------------------
+def quantize_scale(digits: int) -> float:
+    """The power-of-two scale of quantize.py:65-73."""
+    precision = 10.0**-digits
+    exp = math.log10(precision)
+    exp = math.floor(exp) if exp < 0 else math.ceil(exp)
+    bits = math.ceil(math.log2(10.0**-exp))
+    return 2.0**bits
+
+
+def quantize_encode(buf, digits, dtype, astype=None) -> np.ndarray:
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    arr = np.asarray(buf).view(dtype)
+    scale = quantize_scale(digits)
+    enc = np.around(scale * arr) / scale
+    return enc.astype(astype, copy=False)
+
+
+def quantize_decode(buf, dtype, astype=None) -> np.ndarray:
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    return np.asarray(buf).view(astype).astype(dtype, copy=False)
+
+
+# --------------------------------------------------------------------------
+# FixedScaleOffset: fixedscaleoffset.py:83-113
+# --------------------------------------------------------------------------
+def fso_encode(buf, offset, scale, dtype, astype=None) -> np.ndarray:
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    arr = np.asarray(buf).view(dtype).reshape(-1, order="A")
+    enc = np.around((arr - offset) * scale)
+    return enc.astype(astype, copy=False)
+
+
+def fso_decode(buf, offset, scale, dtype, astype=None) -> np.ndarray:
+    dtype = np.dtype(dtype)
+    astype = dtype if astype is None else np.dtype(astype)
+    enc = np.asarray(buf).view(astype).reshape(-1, order="A")
+    dec = (enc / scale) + offset
+    return dec.astype(dtype, copy=False)
+
+
+# --------------------------------------------------------------------------
+# CPU baseline helpers (bench.py cpu_baseline leg)
+# --------------------------------------------------------------------------
+def shuffle_into(src: np.ndarray, dst: np.ndarray, elementsize: int) -> None:
+    _c().nco_shuffle(_ptr(src), _ptr(dst), src.nbytes, elementsize)
+
+
+def unshuffle_into(src: np.ndarray, dst: np.ndarray, elementsize: int) -> None:
+    _c().nco_unshuffle(_ptr(src), _ptr(dst), src.nbytes, elementsize)
