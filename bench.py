@@ -1,0 +1,314 @@
+"""Benchmark: Shuffle(4) encode+decode of device-resident 256 MiB fp32 chunks.
+
+Metric (BASELINE.json): "GiB/s encode+decode per GPU, device-resident fp32
+chunks (Shuffle, BitRound)", measured on configs[1]: Shuffle(elementsize=4)
+on a 256 MiB float32 chunk per GPU.  One step = Shuffle(4).encode +
+Shuffle(4).decode of one chunk (4 rotating buffer sets per GPU so that the
+256 MiB Infinity Cache cannot serve a step from the previous one).
+value = (bytes into encode + bytes into decode) over all ranks / time.
+
+    python bench.py [--gpus N --steps K --warmup W] [--no-cpu] [--extra]
+
+For N > 1 the driver launches one process per GPU with torch.distributed.run;
+chunks are independent, so every rank streams its own chunks (weak scaling)
+and the only collectives are the timing barrier and the max-over-ranks of
+the elapsed time (no data-path collective).
+
+Printed (rank 0): ONE JSON line with the contract's keys plus
+  roofline     -- the encode kernel: algorithmic bytes per launch (2 x 256 MiB)
+                  / its mean launch duration from HIP events recorded on its
+                  stream inside the timed region; peak 8 TB/s; `traffic` =
+                  HBM bytes per launch from rocprofv3 PMC counters committed
+                  under profiles/ (null when absent);
+  cpu_baseline -- the reference's own Cython _doShuffle/_doUnshuffle
+                  (src/numcodecs/_shuffle.pyx, compiled from the reference
+                  sources into oracle/_ref by oracle/build_ref.sh) on one host
+                  core, time-bounded sample of the same workload; falls back to
+                  the oracle's C restatement ("port") when _ref is absent.
+"""
+
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MiB = 1 << 20
+GiB = 1 << 30
+CHUNK = 256 * MiB
+PEAK_GBPS = 8000.0  # MI355X HBM3E peak, 8.0 TB/s (MI355X_MICROARCH.md)
+METRIC = "GiB/s encode+decode per GPU, device-resident fp32 chunks (Shuffle, BitRound)"
+
+
+def dist_setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+        return dist, rank, world, local
+    return None, 0, 1, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        if torch.cuda.is_available():
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(dist, value: float) -> float:
+    if dist is None:
+        return value
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic():
+    """HBM bytes per encode launch from the newest profiles/*/pmc_summary.json
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per launch)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get("shuffle_enc")
+    if not k:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def cpu_baseline(seconds: float = 10.0):
+    """Reference Shuffle(4) enc+dec on one core, time-bounded sample."""
+    x = np.random.default_rng(0).integers(0, 256, CHUNK, dtype=np.uint8)
+    enc = np.empty_like(x)
+    dec = np.empty_like(x)
+    kind = "port"
+    try:
+        from oracle import refload
+
+        if not os.path.isdir(refload.REF_BUILD) or not glob.glob(os.path.join(refload.REF_BUILD, "_shuffle*.so")):
+            raise ImportError
+        import importlib.util
+
+        so = glob.glob(os.path.join(refload.REF_BUILD, "_shuffle*.so"))[0]
+        spec = importlib.util.spec_from_file_location("numcodecs._shuffle", so)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        do_enc, do_dec = mod._doShuffle, mod._doUnshuffle
+        kind = "reference"
+        src_desc = "src/numcodecs/_shuffle.pyx _doShuffle/_doUnshuffle compiled from the reference sources (oracle/_ref)"
+    except Exception:
+        from oracle import nporacle
+
+        def do_enc(a, b, es):
+            nporacle.shuffle_into(a, b, es)
+
+        def do_dec(a, b, es):
+            nporacle.unshuffle_into(a, b, es)
+
+        src_desc = "oracle/ncoracle.c restatement of _shuffle.pyx:11-30 (-O3, no -march)"
+    do_enc(x, enc, 4)  # warm
+    do_dec(enc, dec, 4)
+    assert np.array_equal(dec, x)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        do_enc(x, enc, 4)
+        do_dec(enc, dec, 4)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 3:
+            break
+    gibps = 2 * CHUNK * n / GiB / el
+    return {
+        "value": round(gibps, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"Shuffle(4) encode+decode of one 256 MiB chunk x {n} ({el:.1f} s), {src_desc}",
+    }
+
+
+def run_step_timing(args, dev, dist, rank, world):
+    from numcodecs_amd import Shuffle
+
+    codec = Shuffle(4)
+    sets = 4
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    ins = [torch.randn(CHUNK // 4, generator=g, device=dev, dtype=torch.float32) for _ in range(sets)]
+    encs = [torch.empty(CHUNK, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    decs = [torch.empty(CHUNK, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    # parity gate before timing: decode(encode(x)) == x on every set
+    for i in range(sets):
+        codec.encode(ins[i], out=encs[i])
+        codec.decode(encs[i], out=decs[i])
+        assert torch.equal(decs[i].view(torch.float32), ins[i]), "round trip failed"
+
+    def step(i):
+        codec.encode(ins[i % sets], out=encs[i % sets])
+        codec.decode(encs[i % sets], out=decs[i % sets])
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    # per-launch HIP events on the stream the kernels run on (torch's current)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[3 * i].record()
+        codec.encode(ins[i % sets], out=encs[i % sets])
+        ev[3 * i + 1].record()
+        codec.decode(encs[i % sets], out=decs[i % sets])
+        ev[3 * i + 2].record()
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    enc_ms = [ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.steps)]
+    dec_ms = [ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)]
+    return elapsed, float(np.mean(enc_ms)), float(np.mean(dec_ms))
+
+
+def extra_workloads(dev):
+    """The other configurations of BASELINE.json, single GPU (reported under
+    "extra", not the headline value)."""
+    from numcodecs_amd import BitRound, Delta, FixedScaleOffset, Shuffle, batch
+
+    out = {}
+
+    def timed(fn, reps=20):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    x32 = torch.randn(CHUNK // 4, device=dev)
+    # C2 f64 Shuffle(8)
+    x64 = torch.randn(CHUNK // 8, device=dev, dtype=torch.float64)
+    e64 = Shuffle(8).encode(x64)
+    t = timed(lambda: Shuffle(8).decode(Shuffle(8).encode(x64, out=e64)))
+    out["C2_shuffle8_f64_encdec_GiBps"] = round(2 * CHUNK / GiB / t, 1)
+    # C3 BitRound(10) fused with Shuffle(4); decode = unshuffle (+ re-view)
+    pipe = batch.FilterPipeline([BitRound(10), Shuffle(4)])
+    enc = pipe.encode(x32)
+    t_e = timed(lambda: pipe.encode(x32))
+    t_d = timed(lambda: Shuffle(4).decode(enc))
+    out["C3_bitround10_shuffle4_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
+    # C4 FSO(f4->i2) -> Delta(i2) -> Shuffle(2)
+    xc = 1000.0 + 10.0 * torch.rand(CHUNK // 4, device=dev)
+    fso = FixedScaleOffset(offset=1000, scale=1e3, dtype="<f4", astype="<i2")
+    dl = Delta(dtype="<i2")
+    sh = Shuffle(2)
+    e = sh.encode(dl.encode(fso.encode(xc)))
+    t_e = timed(lambda: sh.encode(dl.encode(fso.encode(xc))))
+    t_d = timed(lambda: fso.decode(dl.decode(sh.decode(e))))
+    out["C4_fso_delta_shuffle2_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
+    del xc, e, x64, e64
+    # C5 batch 8192 x 1 MiB Shuffle(4) + Fletcher32, one GPU
+    xb = torch.randint(0, 256, (8192, MiB), dtype=torch.uint8, device=dev)
+    eb = batch.shuffle_fletcher32_encode_chunks(xb, 4)
+    db = torch.empty_like(xb)
+    t_e = timed(lambda: batch.shuffle_fletcher32_encode_chunks(xb, 4, out=eb), reps=5)
+    t_d = timed(lambda: batch.fletcher32_unshuffle_decode_chunks(eb, MiB, 4, out=db, check_sums=False), reps=5)
+    out["C5_batch8192x1MiB_shuffle4_fletcher32_encdec_GiBps"] = round(2 * 8192 * MiB / GiB / (t_e + t_d), 1)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--extra", action="store_true", help="also time C2(f64)/C3/C4/C5 on rank 0")
+    args = ap.parse_args()
+
+    dist, rank, world, local = dist_setup(args.gpus)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    elapsed, enc_ms, dec_ms = run_step_timing(args, dev, dist, rank, world)
+    t = max_over_ranks(dist, elapsed)
+    enc_ms = max_over_ranks(dist, enc_ms)
+    dec_ms = max_over_ranks(dist, dec_ms)
+    total_bytes = world * args.steps * 2 * CHUNK  # bytes into encode + decode, all ranks
+    value = total_bytes / GiB / t
+
+    result = None
+    if rank == 0:
+        achieved = 2 * CHUNK / (enc_ms * 1e-3) / 1e9  # GB/s, encode kernel
+        traffic, traffic_src = pmc_traffic()
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randn fp32 on device, 4 rotating 256 MiB chunk sets per GPU)",
+            "config": {
+                "workload": "configs[1]: Shuffle(elementsize=4) encode+decode, one 256 MiB fp32 chunk per GPU per step",
+                "chunk_bytes": CHUNK,
+                "elementsize": 4,
+                "parallelism": f"chunk-sharded x{world} (no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_shuffle_enc<4> (Shuffle(4).encode, 2 x 256 MiB algorithmic bytes/launch)",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_GBPS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "decode_kernel_GBps": round(2 * CHUNK / (dec_ms * 1e-3) / 1e9, 1),
+                "encode_ms": round(enc_ms, 4),
+                "decode_ms": round(dec_ms, 4),
+            },
+        }
+    if rank == 0 and args.extra:
+        result["extra"] = extra_workloads(dev)
+    if rank == 0:
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        barrier(dist)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -171,10 +171,18 @@ def available() -> bool:
     return torch.cuda.is_available()
 
 
+_device_ok = False
+
+
 def require_device() -> None:
     """Fail loudly when there is no HIP device: no CPU fallback exists."""
+    global _device_ok
+    if _device_ok:
+        return
     _load()
-    if not torch.cuda.is_available():
+    if torch.cuda.is_available():
+        _device_ok = True
+    else:
         raise MCodecError(
             "numcodecs_amd requires a HIP device (MI355X/gfx950); none is visible. "
             "There is no CPU fallback in the product path."

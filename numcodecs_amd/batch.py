@@ -93,7 +93,7 @@ def fletcher32_chunks(chunks, nbytes=None) -> torch.Tensor:
             check(lib.mc_fletcher32_batch(rows.data_ptr(), rows.stride(0), b, nbytes, res.data_ptr(),
                                           ws.data_ptr(), ws.numel(), _ops.stream(rows)),
                   "mc_fletcher32_batch")
-    return res.view(torch.uint32).to(torch.int64) if b else res.to(torch.int64)
+    return res.to(torch.int64) & 0xFFFFFFFF
 
 
 def shuffle_fletcher32_encode_chunks(chunks, elementsize, out=None):
@@ -136,7 +136,7 @@ def fletcher32_unshuffle_decode_chunks(encoded, chunk_bytes, elementsize, out=No
                 elementsize, status.data_ptr(), ws.data_ptr(), ws.numel(), _ops.stream(rows)),
                 "mc_fletcher32_unshuffle_batch")
     if check_sums and b:
-        st = status.view(torch.uint32).to(torch.int64)
+        st = status.to(torch.int64) & 0xFFFFFFFF
         bad = (st[:, 0] != st[:, 1]).nonzero()
         if bad.numel():
             i = int(bad[0, 0])

@@ -77,7 +77,17 @@ MC_DEV McNum mc_num_cast(McNum v, int from, int to) {
     const double x = v.f;
     switch (to) {
       case MC_I8: return mc_num_i(mc_cvtt_i64(x));
-      case MC_U4: return mc_num_i(mc_wrap(mc_cvtt_i64(x), MC_U4));
+      case MC_U4: {
+        // numpy's vectorised x86-64 loop (cvttpd2dq/cvttps2dq with the
+        // 2^31 bias trick), which converts every element of a chunk except
+        // the scalar remainder of the SIMD loop; numpy's scalar remainder
+        // truncates a 64-bit conversion instead, so numpy itself is
+        // position-dependent for |x| >= 2^32 ("casts").
+        const uint32_t r = x >= 2147483648.0
+                               ? ((uint32_t)mc_cvtt_i32(x - 2147483648.0) ^ 0x80000000u)
+                               : (uint32_t)mc_cvtt_i32(x);
+        return mc_num_i((int64_t)r);
+      }
       case MC_U8: return mc_num_i((int64_t)mc_cvtt_u64(x));
       default: return mc_num_i(mc_wrap((int64_t)mc_cvtt_i32(x), to));
     }

@@ -1,0 +1,93 @@
+"""Shared checks, restating the behaviour of the reference's test harness
+(tests/common.py:31-243 of numcodecs) for numcodecs_amd codecs."""
+
+from __future__ import annotations
+
+import array
+import json
+import os
+from glob import glob
+
+import numpy as np
+from numpy.testing import assert_array_almost_equal, assert_array_equal
+
+import numcodecs_amd
+from numcodecs_amd import get_codec
+from numcodecs_amd.compat import ensure_bytes, ensure_ndarray
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURE = os.path.join(GOLDEN, "reference_fixture")
+
+
+def compare_arrays(arr, res, precision=None):
+    """common.py:31-48: view `res` as arr.dtype, reshape, compare."""
+    res = np.asarray(ensure_ndarray(res)).view(arr.dtype)
+    res = res.reshape(arr.shape, order="F" if arr.flags.f_contiguous else "C")
+    if precision is None:
+        assert_array_equal(arr, res)
+    else:
+        assert_array_almost_equal(arr, res, decimal=precision)
+
+
+def check_encode_decode(arr, codec, precision=None):
+    """common.py:51-116: round trip through every buffer flavour."""
+    enc = codec.encode(arr)
+    compare_arrays(arr, codec.decode(enc), precision)
+    raw = arr.tobytes(order="A")
+    for buf in (raw, bytearray(raw), array.array("b", raw)):
+        enc = codec.encode(buf)
+        compare_arrays(arr, codec.decode(enc), precision)
+    enc_bytes = ensure_bytes(enc)
+    for buf in (enc_bytes, bytearray(enc_bytes), array.array("b", enc_bytes),
+                np.frombuffer(enc_bytes, dtype="u1")):
+        compare_arrays(arr, codec.decode(buf), precision)
+    out = np.empty_like(arr)
+    codec.decode(enc_bytes, out=out)
+    compare_arrays(arr, out, precision)
+    out = bytearray(arr.nbytes)
+    codec.decode(enc_bytes, out=out)
+    compare_arrays(arr, out, precision)
+
+
+def check_config(codec):
+    """common.py:154-158."""
+    config = json.loads(json.dumps(codec.get_config()))
+    assert codec == get_codec(config)
+
+
+def check_repr(stmt):
+    """common.py:161-165 (names resolved in numcodecs_amd)."""
+    ns = {name: getattr(numcodecs_amd, name) for name in numcodecs_amd.__all__}
+    assert repr(eval(stmt, ns)) == stmt
+
+
+def load_fixture_array(fn):
+    return np.load(fn, allow_pickle=False)
+
+
+def fixture_cases(codec_id, prefix=None):
+    """Yield (arr, j, config, encoded_bytes) for every stored fixture file
+    (common.py:168-243 layout: array.NN.npy, codec.MM/config.json,
+    codec.MM/encoded.NN.dat).  Read-only: nothing is ever written."""
+    d = os.path.join(FIXTURE, codec_id, prefix) if prefix else os.path.join(FIXTURE, codec_id)
+    for arr_fn in sorted(glob(os.path.join(d, "array.*.npy"))):
+        i = int(arr_fn.split(".")[-2])
+        arr = load_fixture_array(arr_fn)
+        for codec_dir in sorted(glob(os.path.join(d, "codec.*"))):
+            j = int(codec_dir.split(".")[-1])
+            with open(os.path.join(codec_dir, "config.json")) as f:
+                config = json.load(f)
+            with open(os.path.join(codec_dir, f"encoded.{i:02d}.dat"), "rb") as f:
+                enc = f.read()
+            yield arr, j, config, enc
+
+
+def load_vectors():
+    with open(os.path.join(GOLDEN, "vectors.json")) as f:
+        manifest = json.load(f)
+    data = np.load(os.path.join(GOLDEN, "vectors.npz"), allow_pickle=False)
+    return manifest, data
+
+
+def vec(data, family, i, key):
+    return data[f"{family}__{i}__{key}"]
