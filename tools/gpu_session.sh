@@ -20,8 +20,15 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=900 -p no:cacheprovider -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    benchprof) run rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o bench -- python3 bench.py ;;
     benchx) run bench_extra 900 python bench.py --extra --no-cpu ;;
     probe) run probe_enc4 600 python tools/probe_enc.py 4 ;;
+    rocprof) run rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
+               -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --steps 50 --warmup 5 ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_fetch -o bench -- python3 bench.py --no-cpu --steps 20 --warmup 2
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_write -o bench -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
