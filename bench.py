@@ -57,8 +57,11 @@ def dist_setup(n_gpus: int):
     if world > 1:
         import torch.distributed as dist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        # RCCL ("nccl") on the GPU node; MCODEC_BENCH_BACKEND=gloo rehearses
+        # several ranks on one GPU (device = LOCAL_RANK mod visible devices)
+        backend = os.environ.get("MCODEC_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            local = local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
         return dist, rank, world, local
@@ -67,7 +70,7 @@ def dist_setup(n_gpus: int):
 
 def barrier(dist):
     if dist is not None:
-        if torch.cuda.is_available():
+        if torch.cuda.is_available() and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
@@ -76,7 +79,8 @@ def barrier(dist):
 def max_over_ranks(dist, value: float) -> float:
     if dist is None:
         return value
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    on_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -243,6 +247,46 @@ def extra_workloads(dev):
     return out
 
 
+def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
+    """Host -> host rate: pinned H2D + Shuffle(4) kernel + D2H, pipelined over
+    3 streams (batch.host_pipeline); reported under "end_to_end"."""
+    from numcodecs_amd import batch
+
+    nchunks = total_gib * GiB // chunk_bytes
+    hin = torch.randint(0, 256, (nchunks, chunk_bytes), dtype=torch.uint8).pin_memory()
+    henc = torch.empty_like(hin).pin_memory()
+    hdec = torch.empty_like(hin).pin_memory()
+    res = {}
+    for slice_chunks in (16, 64):
+        batch.host_pipeline(hin, henc, 4, True, slice_chunks=slice_chunks)
+        t0 = time.perf_counter()
+        batch.host_pipeline(hin, henc, 4, True, slice_chunks=slice_chunks)
+        te = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        batch.host_pipeline(henc, hdec, 4, False, slice_chunks=slice_chunks)
+        td = time.perf_counter() - t0
+        assert torch.equal(hdec, hin)
+        res[f"slice_{slice_chunks * chunk_bytes // MiB}MiB"] = {
+            "encode_GiBps": round(nchunks * chunk_bytes / GiB / te, 2),
+            "decode_GiBps": round(nchunks * chunk_bytes / GiB / td, 2),
+        }
+    # raw PCIe rates for reference: pinned copies alone
+    d = torch.empty((nchunks, chunk_bytes), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d.copy_(hin, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    henc.copy_(d, non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = time.perf_counter() - t0
+    res["pcie_h2d_GiBps"] = round(total_gib / h2d, 2)
+    res["pcie_d2h_GiBps"] = round(total_gib / d2h, 2)
+    res["workload"] = f"{total_gib} GiB of {chunk_bytes // MiB} MiB chunks in pinned host memory, Shuffle(4), host->host"
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -251,6 +295,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true", help="also time C2(f64)/C3/C4/C5 on rank 0")
+    ap.add_argument("--e2e", action="store_true", help="also time the host->host pipelined path")
     args = ap.parse_args()
 
     dist, rank, world, local = dist_setup(args.gpus)
@@ -301,6 +346,8 @@ def main():
         }
     if rank == 0 and args.extra:
         result["extra"] = extra_workloads(dev)
+    if rank == 0 and args.e2e:
+        result["end_to_end"] = end_to_end(dev)
     if rank == 0:
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -37,6 +37,7 @@ __all__ = [
     "shuffle_fletcher32_encode_chunks",
     "fletcher32_unshuffle_decode_chunks",
     "encoded_stride",
+    "host_pipeline",
 ]
 
 
@@ -268,3 +269,45 @@ def _fletcher32_unshuffle(sh: Shuffle, x: torch.Tensor) -> torch.Tensor:
     if v[0] != v[1]:
         raise _mismatch(int(v[0]), int(v[1]))
     return out
+
+
+def host_pipeline(host_in: torch.Tensor, host_out: torch.Tensor, elementsize: int, encode=True,
+                  slice_chunks: int = 64, nstreams: int = 3, device=None) -> None:
+    """Shuffle a batch of chunks that lives in (pinned) host memory.
+
+    The Zarr caller's chunks start and end in host memory (a file or socket
+    buffer).  ``host_in``/``host_out`` are [B, chunk_bytes] uint8 CPU tensors
+    (pin them for asynchronous DMA).  Slices of `slice_chunks` chunks go
+    round-robin over `nstreams` HIP streams as H2D copy -> kernel -> D2H copy,
+    so the two DMA directions and the kernels of different slices overlap;
+    each stream reuses its own device buffers in stream order.  Returns when
+    host_out is complete.
+    """
+    _native.require_device()
+    if host_in.device.type != "cpu" or host_out.device.type != "cpu":
+        raise TypeError("host_pipeline takes CPU tensors (pinned for overlap)")
+    if host_in.shape != host_out.shape or host_in.dim() != 2:
+        raise ValueError("host_in and host_out must be [B, chunk_bytes] of equal shape")
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    b, n = host_in.shape
+    if b == 0 or n == 0:
+        return
+    slice_chunks = max(1, min(slice_chunks, b))
+    with torch.cuda.device(device):
+        streams = [torch.cuda.Stream(device=device) for _ in range(nstreams)]
+        dev_in = [torch.empty((slice_chunks, n), dtype=torch.uint8, device=device) for _ in streams]
+        dev_out = [torch.empty((slice_chunks, n), dtype=torch.uint8, device=device) for _ in streams]
+        cur = torch.cuda.current_stream(device)
+        for s in streams:
+            s.wait_stream(cur)  # buffers were allocated on the current stream
+        for k, lo in enumerate(range(0, b, slice_chunks)):
+            hi = min(b, lo + slice_chunks)
+            i = k % nstreams
+            with torch.cuda.stream(streams[i]):
+                di = dev_in[i][: hi - lo]
+                do = dev_out[i][: hi - lo]
+                di.copy_(host_in[lo:hi], non_blocking=True)
+                _ops.shuffle_batch(di, n, do, n, hi - lo, n, elementsize, encode)
+                host_out[lo:hi].copy_(do, non_blocking=True)
+        for s in streams:
+            s.synchronize()

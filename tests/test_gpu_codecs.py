@@ -461,3 +461,17 @@ def test_pipeline_fusion_matches_sequential(device):
     dec = pipe.decode(enc)
     assert np.array_equal(dec.cpu().numpy().view("f4") if dec.dtype == torch.uint8 else dec.cpu().numpy(),
                           oracle.bitround_encode(xh, 10).view("f4"))
+
+
+def test_host_pipeline_roundtrip(device):
+    """Host-resident chunks: pinned H2D -> kernel -> D2H over 3 streams."""
+    b, n = 37, 4096 * 4 * 2
+    hin = torch.randint(0, 256, (b, n), dtype=torch.uint8).pin_memory()
+    henc = torch.empty_like(hin).pin_memory()
+    hdec = torch.empty_like(hin).pin_memory()
+    batch.host_pipeline(hin, henc, 4, True, slice_chunks=5)
+    xh = hin.numpy()
+    for c in (0, 17, 36):
+        assert np.array_equal(henc[c].numpy(), oracle.shuffle(xh[c], 4))
+    batch.host_pipeline(henc, hdec, 4, False, slice_chunks=7)
+    assert torch.equal(hdec, hin)
