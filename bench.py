@@ -227,15 +227,19 @@ def extra_workloads(dev):
     t_e = timed(lambda: pipe.encode(x32))
     t_d = timed(lambda: Shuffle(4).decode(enc))
     out["C3_bitround10_shuffle4_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
-    # C4 FSO(f4->i2) -> Delta(i2) -> Shuffle(2)
+    # C4 FSO(f4->i2) -> Delta(i2) -> Shuffle(2): fused pipeline, and codec by codec
     xc = 1000.0 + 10.0 * torch.rand(CHUNK // 4, device=dev)
     fso = FixedScaleOffset(offset=1000, scale=1e3, dtype="<f4", astype="<i2")
     dl = Delta(dtype="<i2")
     sh = Shuffle(2)
-    e = sh.encode(dl.encode(fso.encode(xc)))
+    c4 = batch.FilterPipeline([fso, dl, sh])
+    e = c4.encode(xc)
+    t_e = timed(lambda: c4.encode(xc))
+    t_d = timed(lambda: c4.decode(e))
+    out["C4_fso_delta_shuffle2_fused_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
     t_e = timed(lambda: sh.encode(dl.encode(fso.encode(xc))))
     t_d = timed(lambda: fso.decode(dl.decode(sh.decode(e))))
-    out["C4_fso_delta_shuffle2_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
+    out["C4_fso_delta_shuffle2_codec_by_codec_encdec_GiBps"] = round(2 * CHUNK / GiB / (t_e + t_d), 1)
     del xc, e, x64, e64
     # C5 batch 8192 x 1 MiB Shuffle(4) + Fletcher32, one GPU
     xb = torch.randint(0, 256, (8192, MiB), dtype=torch.uint8, device=dev)

@@ -177,6 +177,24 @@ int mc_fletcher32_unshuffle_batch(const void *src, size_t src_stride,
                                   void *workspace, size_t workspace_bytes,
                                   mc_stream_t stream);
 
+/* Per chunk of n elements: Shuffle(itemsize(astype)).encode(
+ *   Delta(astype).encode(FixedScaleOffset(offset, scale, dtype, astype).encode(x)))
+ * in one pass (fixedscaleoffset.py:83-97, delta.py:52-67, _shuffle.pyx:11-18).
+ * dtype in {F4, F8}; astype in {I2, U2, I4, U4}; n % 4 == 0; 16-B aligned
+ * buffers.  offset/scale are the values numpy uses, already converted to
+ * dtype (the host checks that numpy computes FSO in dtype, i.e. the scalars
+ * are weak Python numbers). */
+int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n,
+                                int dtype, int astype, double offset,
+                                double scale, mc_stream_t stream);
+/* Inverse chain: unshuffle, cumsum in astype, (x / scale + offset) in
+ * float64 cast to dtype (fixedscaleoffset.py:99-113, delta.py:69-83). */
+size_t mc_fso_delta_shuffle_decode_workspace(size_t n);
+int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
+                                int astype, int dtype, double scale,
+                                double offset, void *workspace,
+                                size_t workspace_bytes, mc_stream_t stream);
+
 /* ---- tuning / measurement hooks (bench.py) ----------------------------- */
 /* Shuffle with an explicit kernel variant and grid (0 = default); used by
  * bench.py to sweep variants.  variant: 0 default, 1 register/dword stores,

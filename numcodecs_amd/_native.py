@@ -98,6 +98,11 @@ _SIGNATURES = {
     "mc_fletcher32_unshuffle_batch": [
         _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp,
     ],
+    "mc_fso_delta_shuffle_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp],
+    "mc_fso_delta_shuffle_decode_workspace": [_c_size],
+    "mc_fso_delta_shuffle_decode": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
+    ],
     "mc_shuffle_variant": [_c_vp, _c_vp, _c_size, _c_size, _c_int, _c_int, _c_int, _c_vp],
 }
 _RESTYPES = {
@@ -106,6 +111,7 @@ _RESTYPES = {
     "mc_fletcher32_workspace": ctypes.c_size_t,
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
+    "mc_fso_delta_shuffle_decode_workspace": ctypes.c_size_t,
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -26,6 +26,8 @@ from . import _native, _ops
 from ._native import check, lib
 from .bitround import BitRound, max_bits
 from .compat import ensure_contiguous_ndarray, is_device_tensor
+from .delta import Delta
+from .fixedscaleoffset import FixedScaleOffset, _resolve
 from .fletcher32 import Fletcher32, _mismatch
 from .shuffle import Shuffle
 
@@ -187,6 +189,12 @@ class FilterPipeline:
                 x = _shuffle_fletcher32(c, x)
                 i += 2
                 continue
+            if i + 2 < len(cs) and is_device_tensor(x):
+                fused = _fso_delta_shuffle_encode(c, nxt, cs[i + 2], x)
+                if fused is not None:
+                    x = fused
+                    i += 3
+                    continue
             x = c.encode(x)
             i += 1
         return x
@@ -209,11 +217,91 @@ class FilterPipeline:
                 x = _fletcher32_unshuffle(nxt, x)
                 i += 2
                 continue
+            if i + 2 < len(cs) and is_device_tensor(x):
+                fused = _fso_delta_shuffle_decode(cs[i + 2], nxt, c, x)
+                if fused is not None:
+                    x = fused
+                    i += 3
+                    if i == len(cs):
+                        return ndarray_copy(x, out)
+                    continue
             if i == len(cs) - 1:
                 return c.decode(x, out=out)
             x = c.decode(x)
             i += 1
         return ndarray_copy(x, out)
+
+
+_C4_FLOATS = ("<f4", "<f8")
+_C4_INTS = ("<i2", "<u2", "<i4", "<u4")
+
+
+def _c4_scalars(fso, delta, sh):
+    """Scalars of the fused FSO -> Delta -> Shuffle path, or None when the
+    chain is not the one the fused kernels implement (numpy must compute FSO
+    encode in the float dtype and decode in float64)."""
+    if not (isinstance(fso, FixedScaleOffset) and isinstance(delta, Delta) and isinstance(sh, Shuffle)):
+        return None
+    d, a = fso.dtype, fso.astype
+    if d.str not in _C4_FLOATS or a.str not in _C4_INTS:
+        return None
+    if delta.dtype != a or delta.astype != a or sh.elementsize != a.itemsize:
+        return None
+    try:
+        t1, off = _resolve(np.subtract, d, fso.offset)
+        t2, sc = _resolve(np.multiply, t1, fso.scale)
+        t3, sc3 = _resolve(np.true_divide, a, fso.scale)
+        t4, off4 = _resolve(np.add, t3, fso.offset)
+    except Exception:
+        return None
+    if t1 != d or t2 != d or t3 != np.float64 or t4 != np.float64:
+        return None
+    return float(off), float(sc), float(sc3), float(off4)
+
+
+def _c4_raw(x: torch.Tensor):
+    src = ensure_contiguous_ndarray(x)
+    return src.view(torch.uint8) if src.numel() else src.new_empty(0, dtype=torch.uint8)
+
+
+def _fso_delta_shuffle_encode(fso, delta, sh, x):
+    sc4 = _c4_scalars(fso, delta, sh)
+    if sc4 is None:
+        return None
+    raw = _c4_raw(x)
+    n, rem = divmod(raw.numel(), fso.dtype.itemsize)
+    if rem or n == 0 or n % 4 or raw.data_ptr() % 16:
+        return None
+    off, sc, _, _ = sc4
+    out = torch.empty(n * fso.astype.itemsize, dtype=torch.uint8, device=raw.device)
+    _native.require_device()
+    with torch.cuda.device(raw.device):
+        check(lib.mc_fso_delta_shuffle_encode(raw.data_ptr(), out.data_ptr(), n,
+                                              _ops.dtype_code(fso.dtype), _ops.dtype_code(fso.astype),
+                                              off, sc, _ops.stream(raw)), "mc_fso_delta_shuffle_encode")
+    return out
+
+
+def _fso_delta_shuffle_decode(fso, delta, sh, x):
+    sc4 = _c4_scalars(fso, delta, sh)
+    if sc4 is None:
+        return None
+    raw = _c4_raw(x)
+    n, rem = divmod(raw.numel(), fso.astype.itemsize)
+    if rem or n == 0 or n % 4 or raw.data_ptr() % 16:
+        return None
+    _, _, sc3, off4 = sc4
+    out = torch.empty(n * fso.dtype.itemsize, dtype=torch.uint8, device=raw.device)
+    _native.require_device()
+    with torch.cuda.device(raw.device):
+        ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_workspace(n), raw)
+        check(lib.mc_fso_delta_shuffle_decode(raw.data_ptr(), out.data_ptr(), n,
+                                              _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype),
+                                              sc3, off4, ws.data_ptr(), ws.numel(), _ops.stream(raw)),
+              "mc_fso_delta_shuffle_decode")
+    from .compat import torch_dtype
+
+    return out.view(torch_dtype(fso.dtype))
 
 
 def _bitround_shuffle(br: BitRound, x: torch.Tensor) -> torch.Tensor:

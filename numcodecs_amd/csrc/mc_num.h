@@ -21,8 +21,8 @@ struct McNum {
   int64_t i;
 };
 
-MC_DEV McNum mc_num_f(double f) { McNum r; r.f = f; r.i = 0; return r; }
-MC_DEV McNum mc_num_i(int64_t i) { McNum r; r.f = 0.0; r.i = i; return r; }
+MC_HD McNum mc_num_f(double f) { McNum r; r.f = f; r.i = 0; return r; }
+MC_HD McNum mc_num_i(int64_t i) { McNum r; r.f = 0.0; r.i = i; return r; }
 
 // wrap a 64-bit integer to dtype width (sign- or zero-extend back to 64 bits)
 MC_DEV int64_t mc_wrap(int64_t v, int dt) {

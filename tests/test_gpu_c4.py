@@ -1,0 +1,77 @@
+"""Fused FixedScaleOffset -> Delta -> Shuffle (BASELINE configs[3]) on the
+GPU: the fused kernels (csrc/mc_c4.hip) must equal the codecs applied one by
+one (which tests/test_gpu_codecs.py pins to the reference) bit for bit, and
+the full-size chain must reproduce the reference's SHA-256 digests."""
+
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import inputs
+import oracle
+from numcodecs_amd import Delta, FixedScaleOffset, Shuffle, batch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _chain(dt, at, offset, scale):
+    fso = FixedScaleOffset(offset=offset, scale=scale, dtype=dt, astype=at)
+    return [fso, Delta(dtype=at), Shuffle(np.dtype(at).itemsize)]
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("at", ["<i2", "<u2", "<i4", "<u4"])
+@pytest.mark.parametrize("n", [4, 4096, 4096 * 5 + 12, 100000])
+def test_fused_equals_sequential(device, dt, at, n):
+    rng = np.random.default_rng(n)
+    x = (1000.0 + rng.uniform(-15, 15, n)).astype(dt)
+    codecs = _chain(dt, at, 1000, 1e3 if np.dtype(at).itemsize == 2 else 1e6)
+    pipe = batch.FilterPipeline(codecs)
+    xd = torch.from_numpy(x).to(device)
+    fused = pipe.encode(xd)
+    seq = xd
+    for c in codecs:
+        seq = c.encode(seq)
+    assert torch.equal(fused.view(torch.uint8), seq.view(torch.uint8))
+    # against the oracle too
+    with np.errstate(all="ignore"):
+        ref = oracle.shuffle(oracle.delta_encode(oracle.fso_encode(x, 1000, codecs[0].scale, dt, at), at),
+                             np.dtype(at).itemsize)
+    assert np.array_equal(fused.cpu().numpy(), ref)
+    dec = pipe.decode(fused)
+    dseq = seq
+    for c in codecs[::-1]:
+        dseq = c.decode(dseq)
+    assert torch.equal(dec.view(torch.uint8).reshape(-1), dseq.view(torch.uint8).reshape(-1))
+
+
+def test_fusion_is_skipped_when_numpy_computes_elsewhere(device):
+    """A strong numpy float64 offset makes numpy compute a float32 chunk in
+    float64: the pipeline must not use the float32 fused kernel."""
+    x = torch.from_numpy((1000.0 + np.arange(4096) / 7.0).astype("<f4")).to(device)
+    codecs = [FixedScaleOffset(offset=np.float64(1000.1), scale=1e3, dtype="<f4", astype="<i4"),
+              Delta(dtype="<i4"), Shuffle(4)]
+    assert batch._c4_scalars(*codecs) is None
+    enc = batch.FilterPipeline(codecs).encode(x)
+    seq = x
+    for c in codecs:
+        seq = c.encode(seq)
+    assert torch.equal(enc.view(torch.uint8), seq.view(torch.uint8))
+
+
+def test_c4_full_size_fused(device):
+    with open(os.path.join(HERE, "golden", "fullsize.json")) as f:
+        full = json.load(f)["C4"]
+    x = inputs.f32_c4(4, 256 * (1 << 20) // 4)
+    xd = torch.from_numpy(x).to(device)
+    del x
+    pipe = batch.FilterPipeline(_chain("<f4", "<i2", 1000, 1e3))
+    enc = pipe.encode(xd)
+    assert hashlib.sha256(enc.cpu().numpy().tobytes()).hexdigest() == full["shuffle2"]
+    dec = pipe.decode(enc)
+    assert hashlib.sha256(dec.view(torch.uint8).cpu().numpy().tobytes()).hexdigest() == full["decoded"]
