@@ -180,7 +180,7 @@ int mc_fletcher32_unshuffle_batch(const void *src, size_t src_stride,
 /* Per chunk of n elements: Shuffle(itemsize(astype)).encode(
  *   Delta(astype).encode(FixedScaleOffset(offset, scale, dtype, astype).encode(x)))
  * in one pass (fixedscaleoffset.py:83-97, delta.py:52-67, _shuffle.pyx:11-18).
- * dtype in {F4, F8}; astype in {I2, U2, I4, U4}; n % 4 == 0; 16-B aligned
+ * dtype in {F4, F8}; astype in {I2, U2, I4, U4}; n % 16 == 0; 16-B aligned
  * buffers.  offset/scale are the values numpy uses, already converted to
  * dtype (the host checks that numpy computes FSO in dtype, i.e. the scalars
  * are weak Python numbers). */

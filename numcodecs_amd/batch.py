@@ -270,7 +270,7 @@ def _fso_delta_shuffle_encode(fso, delta, sh, x):
         return None
     raw = _c4_raw(x)
     n, rem = divmod(raw.numel(), fso.dtype.itemsize)
-    if rem or n == 0 or n % 4 or raw.data_ptr() % 16:
+    if rem or n == 0 or n % 16 or raw.data_ptr() % 16:
         return None
     off, sc, _, _ = sc4
     out = torch.empty(n * fso.astype.itemsize, dtype=torch.uint8, device=raw.device)
@@ -288,7 +288,7 @@ def _fso_delta_shuffle_decode(fso, delta, sh, x):
         return None
     raw = _c4_raw(x)
     n, rem = divmod(raw.numel(), fso.astype.itemsize)
-    if rem or n == 0 or n % 4 or raw.data_ptr() % 16:
+    if rem or n == 0 or n % 16 or raw.data_ptr() % 16:
         return None
     _, _, sc3, off4 = sc4
     out = torch.empty(n * fso.dtype.itemsize, dtype=torch.uint8, device=raw.device)

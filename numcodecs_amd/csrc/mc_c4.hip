@@ -10,11 +10,16 @@
 //   differences in the integer dtype, and writes the 4 integers as plane
 //   dwords of the shuffled chunk (4x4 byte transpose in registers).
 //   HBM: read 4 (or 8) B + write 2 (or 4) B per element.
-// decode, three passes over 4096-element tiles (mc_scan.h): per-tile totals
-//   of the unshuffled deltas; exclusive scan of the totals (one workgroup);
-//   rescan of each tile + FSO decode ((x / scale + offset) in float64, then
-//   cast to the float dtype) + store.  HBM: read 2 B twice + write 4 B.
+// decode, three passes over 4096-element tiles (mc_scan.h), each thread
+//   owning 16 consecutive elements: per-tile totals of the unshuffled deltas;
+//   exclusive scan of the totals (one workgroup); rescan of each tile + FSO
+//   decode ((x / scale + offset) in float64, then cast to the float dtype),
+//   staged through LDS for coalesced stores.  HBM: read 2 B twice + write
+//   4 B per element.  A single-pass decoupled look-back variant exists for
+//   A/B measurement (MCODEC_C4_VARIANT=2).
 // Bit-exact with the reference sequence of codecs (tests/test_gpu_c4.py).
+#include <stdlib.h>
+
 #include "mc_scan.h"
 #include "mc_shuffle.h"
 
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
 #pragma unroll
   for (int q = 0; q < MC_SCAN_STEPS; ++q) {
     const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
-    if (e >= p.n) continue;  // n % 4 == 0: quads are whole
+    if (e >= p.n) continue;  // n % 16 == 0: quads are whole
     uint64_t x[4];
     mc_load4(src + e * DS, DS, x);
     int64_t a[4], d[4];
@@ -99,13 +104,26 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
   }
 }
 
+// A thread owns 16 consecutive elements of a 4096-element tile: one 16-B
+// (lane-contiguous) load per plane, 4 quads unshuffled in registers.
+constexpr int C4_PER = 16;
+
 template <int A, int ES>
-MC_DEV void load_deltas(const uint8_t *src, size_t n, size_t e, int64_t (&d)[4]) {
-  uint32_t pl[ES], w[ES];
+MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)[C4_PER]) {
+  mc_u32x4 pl[ES];
 #pragma unroll
-  for (int b = 0; b < ES; ++b) pl[b] = mc_ld4<true>(src + (size_t)b * n + e);
-  mc_planes_to_quad<ES>(pl, w);
-  unpack_quad<A, ES>(w, d);
+  for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<true>(src + (size_t)b * n + e0);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {  // dword c of every plane = elements 4c..4c+3
+    uint32_t pq[ES], w[ES];
+#pragma unroll
+    for (int b = 0; b < ES; ++b) pq[b] = pl[b][c];
+    mc_planes_to_quad<ES>(pq, w);
+    int64_t d[4];
+    unpack_quad<A, ES>(w, d);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[4 * c + k] = (uint32_t)d[k];
+  }
 }
 
 template <int D, int A>
@@ -113,19 +131,59 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_reduce(const uint8_t *__restric
                                                        uint64_t *__restrict__ sums, C4Params p) {
   constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
   __shared__ uint64_t lds[MC_BLOCK / 64];
-  const size_t tile_e0 = (size_t)blockIdx.x * MC_SCAN_TILE;
-  uint64_t acc = 0;
+  const size_t e0 = (size_t)blockIdx.x * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t acc = 0;
+  if (e0 < p.n) {
+    uint32_t v[C4_PER];
+    load16_deltas<A, ES>(src, p.n, e0, v);
 #pragma unroll
-  for (int q = 0; q < MC_SCAN_STEPS; ++q) {
-    const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
-    if (e >= p.n) continue;
-    int64_t d[4];
-    load_deltas<A, ES>(src, p.n, e, d);
-    acc += (uint64_t)(d[0] + d[1] + d[2] + d[3]);
+    for (int k = 0; k < C4_PER; ++k) acc += v[k];
   }
   uint64_t tot;
   mc_block_excl_scan<false>(acc, lds, &tot);
-  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+  if (threadIdx.x == 0) sums[blockIdx.x] = (uint32_t)tot;
+}
+
+// scan of 16 consecutive deltas + FSO decode, staged through LDS for
+// lane-contiguous 16-B stores; `pre` = exclusive prefix of the thread
+template <int D, int A>
+MC_DEV void c4_finish(uint8_t *dst, size_t tile, const uint32_t (&incl)[C4_PER], uint32_t pre,
+                      uint8_t *outb, const C4Params &p) {
+  constexpr int DS = D == MC_F4 ? 4 : 8;
+#pragma unroll
+  for (int k = 0; k < C4_PER; ++k) {
+    const uint64_t o = fso_dec<D, A>(mc_wrap((int64_t)(uint32_t)(pre + incl[k]), A), p);
+    if constexpr (DS == 4) reinterpret_cast<uint32_t *>(outb)[threadIdx.x * C4_PER + k] = (uint32_t)o;
+    else reinterpret_cast<uint64_t *>(outb)[threadIdx.x * C4_PER + k] = o;
+  }
+  __syncthreads();
+  const size_t tile_b0 = tile * (size_t)MC_SCAN_TILE * DS;
+  const size_t nbytes = p.n * DS;
+#pragma unroll
+  for (int r = 0; r < MC_SCAN_TILE * DS / 16 / MC_BLOCK; ++r) {
+    const size_t off = ((size_t)r * MC_BLOCK + threadIdx.x) * 16;
+    if (tile_b0 + off < nbytes)
+      mc_st16<true>(dst + tile_b0 + off, reinterpret_cast<const mc_u32x4 *>(outb)[r * MC_BLOCK + threadIdx.x]);
+  }
+}
+
+template <int D, int A>
+MC_DEV void c4_local_scan(const uint8_t *src, size_t tile, const C4Params &p, uint32_t (&v)[C4_PER],
+                          uint32_t &run) {
+  constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
+  const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  if (e0 < p.n) {
+    load16_deltas<A, ES>(src, p.n, e0, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+  }
+  run = 0;
+#pragma unroll
+  for (int k = 0; k < C4_PER; ++k) {
+    run += v[k];
+    v[k] = run;
+  }
 }
 
 template <int D, int A>
@@ -133,41 +191,50 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict
                                                       uint8_t *__restrict__ dst,
                                                       const uint64_t *__restrict__ sums,
                                                       C4Params p) {
-  constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
   constexpr int DS = D == MC_F4 ? 4 : 8;
-  __shared__ uint64_t lds[MC_BLOCK / 64];
-  const size_t tile_e0 = (size_t)blockIdx.x * MC_SCAN_TILE;
-  uint64_t carry = sums[blockIdx.x];
-#pragma unroll
-  for (int q = 0; q < MC_SCAN_STEPS; ++q) {
-    const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
-    const bool live = e < p.n;
-    int64_t d[4] = {0, 0, 0, 0};
-    if (live) load_deltas<A, ES>(src, p.n, e, d);
-    uint64_t pr[4], run = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      run += (uint64_t)d[k];
-      pr[k] = run;
-    }
-    uint64_t tot;
-    const uint64_t excl = mc_block_excl_scan<false>(run, lds, &tot);  // all threads
-    if (live) {
-      const uint64_t pre = carry + excl;
-      uint64_t o[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = fso_dec<D, A>(mc_wrap((int64_t)(pre + pr[k]), A), p);
-      if constexpr (DS == 4) {
-        mc_st16<true>(dst + e * 4, mc_u32x4{(uint32_t)o[0], (uint32_t)o[1], (uint32_t)o[2], (uint32_t)o[3]});
-      } else {
-        mc_st16<true>(dst + e * 8, mc_u32x4{(uint32_t)o[0], (uint32_t)(o[0] >> 32), (uint32_t)o[1],
-                                            (uint32_t)(o[1] >> 32)});
-        mc_st16<true>(dst + e * 8 + 16, mc_u32x4{(uint32_t)o[2], (uint32_t)(o[2] >> 32),
-                                                 (uint32_t)o[3], (uint32_t)(o[3] >> 32)});
-      }
-    }
-    carry += tot;
+  __shared__ uint64_t red[MC_BLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
+  const size_t tile = blockIdx.x;
+  uint32_t v[C4_PER], run;
+  c4_local_scan<D, A>(src, tile, p, v, run);
+  uint64_t agg;
+  const uint32_t excl = (uint32_t)mc_block_excl_scan<false>(run, red, &agg);
+  c4_finish<D, A>(dst, tile, v, (uint32_t)sums[tile] + excl, outb, p);
+}
+
+// Single-pass decode with decoupled look-back (mc_scan.h): tiles numbered in
+// start order, the tile's aggregate published right after its block scan,
+// wave 0 walks back 64 predecessors per round.
+template <int D, int A>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_decode_lb(const uint8_t *__restrict__ src,
+                                                          uint8_t *__restrict__ dst,
+                                                          uint32_t *ctrl, uint64_t *status,
+                                                          C4Params p) {
+  constexpr int DS = D == MC_F4 ? 4 : 8;
+  __shared__ uint64_t red[MC_BLOCK / 64];
+  __shared__ uint32_t slot;
+  __shared__ uint32_t prefix_slot;
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
+  const size_t tile = mc_lb_tile(ctrl, &slot);
+  uint32_t v[C4_PER], run;
+  c4_local_scan<D, A>(src, tile, p, v, run);
+  uint64_t agg;
+  const uint32_t excl = (uint32_t)mc_block_excl_scan<false>(run, red, &agg);
+  if (threadIdx.x < 64) {
+    const uint32_t pre = mc_lb_lookback_wave<false>(status, tile, (uint32_t)agg, ctrl + 1);
+    if (threadIdx.x == 0) prefix_slot = pre;
   }
+  __syncthreads();
+  c4_finish<D, A>(dst, tile, v, prefix_slot + excl, outb, p);
+}
+
+template <int D, int A>
+static void c4_decode_lb(const uint8_t *s, uint8_t *d, uint8_t *ws, const C4Params &p,
+                         hipStream_t st) {
+  const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  hipMemsetAsync(ws, 0, mc_lb_workspace(ntiles), st);
+  k_c4_decode_lb<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(
+      s, d, reinterpret_cast<uint32_t *>(ws), reinterpret_cast<uint64_t *>(ws + 16), p);
 }
 
 template <int D, int A>
@@ -185,10 +252,21 @@ static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Para
   k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, sums, p);
 }
 
+// MCODEC_C4_VARIANT=2 selects the single-pass look-back decode (A/B
+// measurement; the three-pass decode is the default)
+static int mc_c4_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("MCODEC_C4_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 static bool c4_ok(const void *src, const void *dst, size_t n, int dtype, int astype) {
   if (!(dtype == MC_F4 || dtype == MC_F8)) return false;
   if (!(astype == MC_I2 || astype == MC_U2 || astype == MC_I4 || astype == MC_U4)) return false;
-  if (n % 4 != 0) return false;
+  if (n % 16 != 0) return false;  // 16-B plane accesses (decode)
   return src && dst && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
 }
 
@@ -231,7 +309,8 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
 }
 
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n) {
-  return ((n + MC_SCAN_TILE - 1) / MC_SCAN_TILE) * sizeof(uint64_t);
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  return mc_lb_workspace(ntiles) > ntiles * 8 ? mc_lb_workspace(ntiles) : ntiles * 8;
 }
 
 int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype, int dtype,
@@ -246,9 +325,14 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype
   p.sc = mc_num_f(scale);
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
-  uint64_t *sums = static_cast<uint64_t *>(workspace);
   hipStream_t st = (hipStream_t)stream;
-  MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
+  if (n % 16 == 0 && mc_c4_variant() == 2) {
+    uint8_t *ws = static_cast<uint8_t *>(workspace);
+    MC_C4_DISPATCH(c4_decode_lb, s, d, ws, p, st);
+  } else {
+    uint64_t *sums = static_cast<uint64_t *>(workspace);
+    MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
+  }
   return mc_last_launch();
 }
 
