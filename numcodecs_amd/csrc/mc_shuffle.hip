@@ -170,6 +170,84 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec(
 }
 
 // ---------------------------------------------------------------------------
+// es = 8 with lane pairs: every lane moves 16 B per access on the element side
+// (2 elements, lane-contiguous: 1 KiB per wave instruction).  Lanes 2m and
+// 2m+1 hold elements 4m..4m+1 and 4m+2..4m+3; one __shfl_xor(., 1) exchange
+// gives the even lane the low dwords and the odd lane the high dwords of the
+// 4 elements, and a 4x4 byte transpose turns them into plane dwords 0-3 (even)
+// and 4-7 (odd).  A plane store instruction therefore writes two 128-B runs.
+// Tile = 256 lanes x NV 16-B units.
+// ---------------------------------------------------------------------------
+template <bool BITROUND, bool NT, int NV>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
+    McBitRound br) {
+  constexpr int TB = NV * 16 * MC_BLOCK, TE = TB / 8;
+  const int tid = threadIdx.x;
+  const bool odd = tid & 1;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)TE;
+    mc_u32x4 v[NV];
+#pragma unroll
+    for (int r = 0; r < NV; ++r) v[r] = mc_ld16<NT>(s + ((size_t)r * MC_BLOCK + tid) * 16);
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      mc_u32x4 x = v[r];
+      if constexpr (BITROUND) {
+        uint64_t e0 = mc_bitround64(((uint64_t)x.y << 32) | x.x, br);
+        uint64_t e1 = mc_bitround64(((uint64_t)x.w << 32) | x.z, br);
+        x = mc_u32x4{(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32)};
+      }
+      const uint32_t a = __shfl_xor(odd ? x.x : x.y, 1, 64);
+      const uint32_t b = __shfl_xor(odd ? x.z : x.w, 1, 64);
+      uint32_t p0, p1, p2, p3;
+      if (odd) mc_tr4(a, b, x.y, x.w, p0, p1, p2, p3);   // high dwords of e0..e3
+      else mc_tr4(x.x, x.z, a, b, p0, p1, p2, p3);       // low dwords of e0..e3
+      const size_t e = (size_t)r * (16 * MC_BLOCK / 8) + 4 * (size_t)(tid >> 1);
+      uint8_t *pd = d + (odd ? 4 * m.count : 0) + e;
+      mc_st4<NT>(pd, p0);
+      mc_st4<NT>(pd + m.count, p1);
+      mc_st4<NT>(pd + 2 * m.count, p2);
+      mc_st4<NT>(pd + 3 * m.count, p3);
+    }
+  }
+}
+
+template <bool NT, int NV>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles) {
+  constexpr int TB = NV * 16 * MC_BLOCK, TE = TB / 8;
+  const int tid = threadIdx.x;
+  const bool odd = tid & 1;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)TE;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)TB;
+    uint32_t pl[NV][4];
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      const size_t e = (size_t)r * (16 * MC_BLOCK / 8) + 4 * (size_t)(tid >> 1);
+      const uint8_t *ps = s + (odd ? 4 * m.count : 0) + e;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pl[r][k] = mc_ld4<NT>(ps + k * m.count);
+    }
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      uint32_t w0, w1, w2, w3;  // even: low dwords of e0..e3; odd: high dwords
+      mc_tr4(pl[r][0], pl[r][1], pl[r][2], pl[r][3], w0, w1, w2, w3);
+      const uint32_t a = __shfl_xor(odd ? w0 : w2, 1, 64);
+      const uint32_t b = __shfl_xor(odd ? w1 : w3, 1, 64);
+      const mc_u32x4 o = odd ? mc_u32x4{a, w2, b, w3} : mc_u32x4{w0, a, w1, b};
+      mc_st16<NT>(d + ((size_t)r * MC_BLOCK + tid) * 16, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // software-pipelined persistent variants (register layout): the next tile's
 // loads are issued before this tile's stores, so waiting for them does not
 // wait for the stores (vmcnt retires loads and stores in issue order).
@@ -318,7 +396,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec_generic(
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4 };
+enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4, V_PAIR = 5 };
 // variant | V_NO_NT selects default-policy (temporal) global accesses
 static constexpr int V_NO_NT = 8;
 // variant | V_BIG selects 2x larger tiles, | V_BIG4 4x (register layout only)
@@ -342,10 +420,8 @@ static int default_variant(size_t es, bool enc, size_t total_bytes, unsigned *gr
   switch (es) {
     case 2: return V_REG | V_BIG4;                       // 6.34 / 6.22 TB/s
     case 4: return enc ? (V_REG | V_BIG4) : (V_REG | V_BIG);  // 6.1 / 6.2 TB/s
-    case 8:
-      if (enc) return V_REG | V_BIG4;                    // 5.4 TB/s
-      *grid_cap = MC_MAX_GRID;
-      return V_BOTH_LDS;                                 // 5.5 TB/s
+    case 8:  // lane pairs keep the 8-B element side lane-contiguous
+      return enc ? V_PAIR : (V_PAIR | V_BIG);            // 5.89 / 6.11 TB/s
     default:
       if (enc) return V_REG | V_BIG;
       *grid_cap = MC_MAX_GRID;
@@ -357,6 +433,14 @@ template <int ES, bool BR, bool NT>
 static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                           size_t ntiles, unsigned grid, const McBitRound &br, hipStream_t st) {
   using G = Geom<ES>;
+  if constexpr (ES == 8) {
+    if ((layout & 7) == V_PAIR) {
+      if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG) k_shuffle8_enc_pair<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else k_shuffle8_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      return;
+    }
+  }
   if (layout == (V_REG | V_PIPE | V_BIG4))
     k_shuffle_enc_pipe<ES, BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
   else if (layout == (V_REG | V_PIPE | V_BIG))
@@ -380,7 +464,8 @@ static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
                             size_t ntiles, unsigned grid, const McBitRound &br,
                             hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
-  if ((layout & 7) < V_REG || (layout & 7) > V_BOTH_LDS) return MC_EINVAL;
+  if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
+  if ((layout & 7) == V_PAIR && ES != 8) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
   else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
   return mc_last_launch();
@@ -390,6 +475,14 @@ template <int ES, bool NT>
 static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                           size_t ntiles, unsigned grid, hipStream_t st) {
   using G = Geom<ES>;
+  if constexpr (ES == 8) {
+    if ((layout & 7) == V_PAIR) {
+      if (layout & V_BIG4) k_shuffle8_dec_pair<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else if (layout & V_BIG) k_shuffle8_dec_pair<NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else k_shuffle8_dec_pair<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      return;
+    }
+  }
   if (layout == (V_REG | V_PIPE | V_BIG4))
     k_shuffle_dec_pipe<ES, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
   else if (layout == (V_REG | V_PIPE | V_BIG))
@@ -412,13 +505,16 @@ template <int ES>
 static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                             size_t ntiles, unsigned grid, hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
-  if ((layout & 7) < V_REG || (layout & 7) > V_BOTH_LDS) return MC_EINVAL;
+  if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
+  if ((layout & 7) == V_PAIR && ES != 8) return MC_EINVAL;
   if (variant & V_NO_NT) launch_dec_nt<ES, false>(layout, s, d, m, ntiles, grid, st);
   else launch_dec_nt<ES, true>(layout, s, d, m, ntiles, grid, st);
   return mc_last_launch();
 }
 
 static size_t tile_elems(size_t es, int variant) {
+  if ((variant & 7) == V_PAIR)  // 256 lanes x NV 16-B units of 8-B elements
+    return (variant & V_BIG4) ? 8192 : (variant & V_BIG) ? 4096 : 2048;
   const size_t te = es >= 16 ? 2048 : 4096;
   if ((variant & 7) != V_REG) return te;
   return (variant & V_BIG4) ? 4 * te : (variant & V_BIG) ? 2 * te : te;
@@ -462,14 +558,17 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
                          (m.src_stride % 16 == 0) && (m.dst_stride % 16 == 0);
   if (!fast_es || !aligned16 || m.count % 4 != 0 || (br && es == 16)) variant = V_GENERIC;
   // the 16-B plane-side accesses need 16-B aligned plane bases
-  if ((variant & 7) != V_GENERIC && (variant & 7) != V_REG && m.count % 16 != 0)
+  if ((variant & 7) != V_GENERIC && (variant & 7) != V_REG && (variant & 7) != V_PAIR &&
+      m.count % 16 != 0)
     variant = V_REG | (variant & (V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE));
 
   size_t e_done = 0;
   McBitRound nobr{};
   const McBitRound &brr = br ? *br : nobr;
   if ((variant & 7) != V_GENERIC) {
-    if ((variant & 7) != V_REG) variant &= ~(V_BIG | V_BIG4 | V_PIPE);
+    if ((variant & 7) == V_PAIR && es != 8) variant = V_REG | (variant & V_NO_NT);
+    if ((variant & 7) != V_REG && (variant & 7) != V_PAIR) variant &= ~(V_BIG | V_BIG4 | V_PIPE);
+    if ((variant & 7) == V_PAIR) variant &= ~V_PIPE;
     if (variant & V_PIPE) variant &= ~V_GROUP_MASK;
     if (variant & V_BIG4) variant &= ~V_BIG;
     m.group = 1u << ((variant & V_GROUP_MASK) >> V_GROUP_SHIFT);
@@ -547,7 +646,7 @@ int mc_unshuffle_batch(const void *src, size_t src_stride, void *dst, size_t dst
 
 int mc_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize,
                        int encode, int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > V_GENERIC ||
+  if (variant < 0 || (variant & 7) > V_PAIR ||
       (variant & ~(7 | V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE)) != 0)
     return MC_EINVAL;
   return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant,

@@ -32,8 +32,9 @@ def main():
     for n in sizes:
         cfgs.append(("copy-nt", n, None, None, 8192))
         for enc in (1, 0):
-            for var, grid in [(v, g) for v in (1, 17, 129, 2, 3) for g in (0, 1024, 4096, 8192, 16384, 32768)] + [
-                    (v, g) for v in (257, 273) for g in (512, 1024, 2048)]:
+            variants = [int(v) for v in os.environ.get("PROBE_VARIANTS", "1,17,129,2,3").split(",")]
+            grids = [int(g) for g in os.environ.get("PROBE_GRIDS", "0,1024,4096,8192,16384,32768").split(",")]
+            for var, grid in [(v, g) for v in variants for g in grids]:
                 cfgs.append(("shuffle", n, enc, var, grid))
     res = {c: [] for c in cfgs}
 
