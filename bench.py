@@ -261,7 +261,7 @@ def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
     henc = torch.empty_like(hin).pin_memory()
     hdec = torch.empty_like(hin).pin_memory()
     res = {}
-    for slice_chunks in (16, 64):
+    for slice_chunks in (16, 32):
         batch.host_pipeline(hin, henc, 4, True, slice_chunks=slice_chunks)
         t0 = time.perf_counter()
         batch.host_pipeline(hin, henc, 4, True, slice_chunks=slice_chunks)
