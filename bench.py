@@ -252,8 +252,8 @@ def extra_workloads(dev):
 
 
 def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
-    """Host -> host rate: pinned H2D + Shuffle(4) kernel + D2H, pipelined over
-    3 streams (batch.host_pipeline); reported under "end_to_end"."""
+    """Host -> host rate: pinned H2D + Shuffle(4) kernel + D2H pipelined over
+    H2D / kernel / D2H role streams (batch.host_pipeline); "end_to_end"."""
     from numcodecs_amd import batch
 
     nchunks = total_gib * GiB // chunk_bytes
