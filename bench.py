@@ -251,6 +251,53 @@ def extra_workloads(dev):
     return out
 
 
+def next_row_workloads(dev):
+    """SURVEY.md §8f next rows (Checksum32 family, PackBits, AsType), single
+    GPU, device-resident; GB/s of algorithmic HBM bytes (read + write) so the
+    numbers compare with the 8 TB/s peak directly."""
+    from numcodecs_amd import AsType, PackBits, batch
+    from numcodecs_amd import _ops
+
+    out = {}
+
+    def timed(fn, reps=10):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    nb = 2048  # 2048 x 1 MiB chunks = 2 GiB per launch
+    xb = torch.randint(0, 256, (nb, MiB), dtype=torch.uint8, device=dev)
+    eb = torch.empty((nb, MiB + 4), dtype=torch.uint8, device=dev)
+    x1 = torch.randint(0, 256, (CHUNK,), dtype=torch.uint8, device=dev)
+    for cid in ("crc32", "crc32c", "adler32"):
+        t = timed(lambda: batch.checksum32_chunks(xb, cid))
+        out[f"{cid}_batch2048x1MiB_checksum_GBps"] = round(nb * MiB / t / 1e9, 1)
+        t = timed(lambda: batch.checksum32_encode_chunks(xb, cid, out=eb))
+        out[f"{cid}_batch2048x1MiB_encode_GBps"] = round(2 * nb * MiB / t / 1e9, 1)
+        kind = batch._CK_KINDS[cid][0]
+        t = timed(lambda: _ops.checksum32(kind, x1, CHUNK, 1, CHUNK, 0))
+        out[f"{cid}_256MiB_checksum_GBps"] = round(CHUNK / t / 1e9, 1)
+    t = timed(lambda: batch.checksum32_chunks(xb, "jenkins_lookup3"), reps=2)
+    out["jenkins_batch2048x1MiB_checksum_GBps"] = round(nb * MiB / t / 1e9, 1)
+    del xb, eb
+    bools = torch.randint(0, 2, (CHUNK,), dtype=torch.uint8, device=dev).view(torch.bool)
+    enc = PackBits().encode(bools)
+    t = timed(lambda: PackBits().encode(bools))
+    out["packbits_256MiB_encode_GBps"] = round((CHUNK + CHUNK // 8) / t / 1e9, 1)
+    t = timed(lambda: PackBits().decode(enc))
+    out["packbits_256MiB_decode_GBps"] = round((CHUNK + CHUNK // 8) / t / 1e9, 1)
+    x64 = torch.randn(CHUNK // 8, device=dev, dtype=torch.float64)
+    t = timed(lambda: AsType("<f4", "<f8").encode(x64))
+    out["astype_f8_to_f4_256MiB_GBps"] = round(1.5 * CHUNK / t / 1e9, 1)
+    return out
+
+
 def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
     """Host -> host rate: pinned H2D + Shuffle(4) kernel + D2H pipelined over
     H2D / kernel / D2H role streams (batch.host_pipeline); "end_to_end"."""
@@ -300,6 +347,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true", help="also time C2(f64)/C3/C4/C5 on rank 0")
     ap.add_argument("--e2e", action="store_true", help="also time the host->host pipelined path")
+    ap.add_argument("--next", action="store_true",
+                    help="also time the SURVEY §8f next rows (checksum32 family, PackBits, AsType)")
     args = ap.parse_args()
 
     dist, rank, world, local = dist_setup(args.gpus)
@@ -352,6 +401,8 @@ def main():
         result["extra"] = extra_workloads(dev)
     if rank == 0 and args.e2e:
         result["end_to_end"] = end_to_end(dev)
+    if rank == 0 and args.next:
+        result["next_rows"] = next_row_workloads(dev)
     if rank == 0:
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

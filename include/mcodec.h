@@ -26,6 +26,12 @@
  *                                    fixedscaleoffset.py:97,110, compat.py:177-206
  *   mc_fletcher32* ................. fletcher32.pyx:24-57 _fletcher32, :75-89 encode,
  *                                    :91-115 decode; _utils.pxd:11-24 store/load_le32
+ *   mc_checksum32_batch /
+ *   mc_checksum32_encode_batch ..... checksum32.py:45-88 Checksum32.encode/decode with
+ *                                    CRC32 (:95-111, zlib.crc32), Adler32 (:114-130,
+ *                                    zlib.adler32), CRC32C (:189-209), JenkinsLookup3
+ *                                    (:133-181 over jenkins.pyx:93-325)
+ *   mc_packbits / mc_unpackbits .... packbits.py:33-82 PackBits.encode/decode
  *   *_batch ........................ no reference counterpart: the Zarr caller loops
  *                                    Codec.encode per chunk; these run B equal-size
  *                                    chunks in one launch (chunk b at base + b*stride).
@@ -194,6 +200,54 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
                                 int astype, int dtype, double scale,
                                 double offset, void *workspace,
                                 size_t workspace_bytes, mc_stream_t stream);
+
+/* ---- Checksum32 family (checksum32.py:45-209, jenkins.pyx:93-325) ------- */
+/* One 32-bit checksum per chunk of a batch (rows at src + c*src_stride):
+ *   MC_CK_CRC32    zlib.crc32(chunk, init)              CRC32.checksum
+ *   MC_CK_CRC32C   crc32c(chunk, init) (Castagnoli)      CRC32C.checksum
+ *   MC_CK_ADLER32  zlib.adler32(chunk, init); the codec passes init = 1.
+ *                  Results are reduced mod 65521, equal to zlib for every
+ *                  init whose halves are both < 65521 (the codec's 1 is)
+ *   MC_CK_JENKINS  jenkins_lookup3(prefix ++ chunk, init); prefix (device
+ *                  bytes, may be NULL when prefix_bytes == 0) only here
+ * out_sums: device uint32[nchunks].  Workspace from mc_checksum32_workspace
+ * (0 for Jenkins, which takes no workspace; pass NULL). */
+enum mc_checksum_kind {
+  MC_CK_CRC32 = 0,
+  MC_CK_CRC32C = 1,
+  MC_CK_ADLER32 = 2,
+  MC_CK_JENKINS = 3
+};
+/* where Checksum32.encode puts the LE32 checksum (checksum32.py:48-62) */
+enum mc_checksum_location { MC_CK_START = 0, MC_CK_END = 1 };
+
+size_t mc_checksum32_workspace(int kind, size_t nchunks, size_t chunk_bytes);
+int mc_checksum32_batch(int kind, const void *src, size_t src_stride,
+                        size_t nchunks, size_t chunk_bytes, uint32_t init,
+                        const void *prefix, size_t prefix_bytes,
+                        uint32_t *out_sums, void *workspace,
+                        size_t workspace_bytes, mc_stream_t stream);
+/* Checksum32.encode of every chunk: dst row c = checksum (LE32) ++ payload
+ * (MC_CK_START) or payload ++ checksum (MC_CK_END); dst_stride >=
+ * chunk_bytes + 4.  The payload copy is fused into the checksum pass
+ * (Jenkins: one hipMemcpy2DAsync).  out_sums may be NULL. */
+int mc_checksum32_encode_batch(int kind, const void *src, size_t src_stride,
+                               void *dst, size_t dst_stride, size_t nchunks,
+                               size_t chunk_bytes, uint32_t init,
+                               const void *prefix, size_t prefix_bytes,
+                               int location, uint32_t *out_sums,
+                               void *workspace, size_t workspace_bytes,
+                               mc_stream_t stream);
+
+/* ---- PackBits (packbits.py:33-82) --------------------------------------- */
+/* encode n bools (any nonzero byte is True) into dst[0] = padding bits
+ * ((8 - n % 8) % 8) followed by np.packbits (MSB first): 1 + ceil(n/8) bytes. */
+int mc_packbits(const void *src, void *dst, size_t n, mc_stream_t stream);
+/* decode: src = the encoded buffer (header byte first, src_bytes long) into
+ * n bools (0/1 bytes); n <= 8 * (src_bytes - 1), normally
+ * 8 * (src_bytes - 1) - src[0] (read by the caller). */
+int mc_unpackbits(const void *src, size_t src_bytes, void *dst, size_t n,
+                  mc_stream_t stream);
 
 /* ---- tuning / measurement hooks (bench.py) ----------------------------- */
 /* Shuffle with an explicit kernel variant and grid (0 = default); used by

@@ -2,12 +2,15 @@
 Instinct MI355X (gfx950).
 
 A drop-in for the hot path of zarr-developers/numcodecs: the codecs
-Shuffle, BitRound, Delta, Quantize, FixedScaleOffset and Fletcher32 with the
-same ids, configs, reprs and error behaviour, executed by hand-written HIP
+Shuffle, BitRound, Delta, Quantize, FixedScaleOffset and Fletcher32 (plus the
+next-row codecs CRC32, CRC32C, Adler32, JenkinsLookup3, AsType and PackBits)
+with the same ids, configs, reprs and error behaviour, executed by hand-written HIP
 kernels (libmcodec.so, C ABI in include/mcodec.h) on device-resident chunks.
 Device tensors stay on the device; host buffers are staged through it.
 
-Reference registrations: src/numcodecs/__init__.py:74,78,82,102,106,127.
+Reference registrations: src/numcodecs/__init__.py:74,78,82,102,106,127
+(the six hot-path codecs), :68-70 AsType, :84-86 PackBits, :108-112 CRC32 /
+Adler32 / JenkinsLookup3, :141-143 CRC32C.
 """
 
 from .abc import Codec
@@ -38,12 +41,33 @@ from .fletcher32 import Fletcher32
 
 register_codec(Fletcher32)
 
+from .checksum32 import CRC32, CRC32C, Adler32, JenkinsLookup3
+
+register_codec(CRC32)
+register_codec(CRC32C)
+register_codec(Adler32)
+register_codec(JenkinsLookup3)
+
+from .astype import AsType
+
+register_codec(AsType)
+
+from .packbits import PackBits
+
+register_codec(PackBits)
+
 from . import batch  # noqa: E402,F401  (batched chunk API and fused pipelines)
 
 __version__ = "0.1.0"
 
 __all__ = [
+    "Adler32",
+    "AsType",
     "BitRound",
+    "CRC32",
+    "CRC32C",
+    "JenkinsLookup3",
+    "PackBits",
     "Codec",
     "Delta",
     "FixedScaleOffset",
@@ -68,7 +92,8 @@ def register_with_numcodecs():
     except Exception:
         return []
     ids = []
-    for cls in (Delta, Quantize, FixedScaleOffset, Shuffle, BitRound, Fletcher32):
+    for cls in (Delta, Quantize, FixedScaleOffset, Shuffle, BitRound, Fletcher32, CRC32, CRC32C,
+                Adler32, JenkinsLookup3, AsType, PackBits):
         _nc_register(cls)
         ids.append(cls.codec_id)
     return ids

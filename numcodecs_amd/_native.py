@@ -61,6 +61,11 @@ _c_int = ctypes.c_int
 _c_vp = ctypes.c_void_p
 _c_double = ctypes.c_double
 _c_i64 = ctypes.c_int64
+_c_u32 = ctypes.c_uint32
+
+# mc_checksum_kind / mc_checksum_location (include/mcodec.h)
+MC_CK_CRC32, MC_CK_CRC32C, MC_CK_ADLER32, MC_CK_JENKINS = 0, 1, 2, 3
+MC_CK_START, MC_CK_END = 0, 1
 
 # name -> argtypes (restype int unless listed in _RESTYPES)
 _SIGNATURES = {
@@ -104,6 +109,16 @@ _SIGNATURES = {
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
     ],
     "mc_shuffle_variant": [_c_vp, _c_vp, _c_size, _c_size, _c_int, _c_int, _c_int, _c_vp],
+    "mc_checksum32_workspace": [_c_int, _c_size, _c_size],
+    "mc_checksum32_batch": [
+        _c_int, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_checksum32_encode_batch": [
+        _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_int,
+        _c_vp, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_packbits": [_c_vp, _c_vp, _c_size, _c_vp],
+    "mc_unpackbits": [_c_vp, _c_size, _c_vp, _c_size, _c_vp],
 }
 _RESTYPES = {
     "mc_strerror": ctypes.c_char_p,
@@ -112,6 +127,7 @@ _RESTYPES = {
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
     "mc_fso_delta_shuffle_decode_workspace": ctypes.c_size_t,
+    "mc_checksum32_workspace": ctypes.c_size_t,
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -181,3 +181,57 @@ def fletcher32(src, nbytes) -> int:
         check(lib.mc_fletcher32(src.data_ptr(), nbytes, out.data_ptr(), ws.data_ptr(), ws.numel(),
                                 stream(src)), "mc_fletcher32")
         return int(out.cpu().numpy().view(np.uint32)[0])
+
+
+# ---------------------------------------------------------------------------
+def _prefix_dev(prefix, like):
+    if prefix is None or len(prefix) == 0:
+        return None
+    if isinstance(prefix, torch.Tensor):
+        return prefix.to(like.device).contiguous().view(torch.uint8)
+    return torch.from_numpy(np.frombuffer(bytes(prefix), dtype=np.uint8).copy()).to(like.device)
+
+
+def checksum32(kind, src, src_stride, nchunks, nbytes, init, prefix=None) -> torch.Tensor:
+    """Checksum of `nchunks` rows of `nbytes` at src + c*src_stride -> device int32[nchunks]
+    (the uint32 values' bit patterns)."""
+    _native.require_device()
+    out = torch.empty(max(nchunks, 1), dtype=torch.int32, device=src.device)
+    with _guard(src):
+        pre = _prefix_dev(prefix, src)
+        ws = workspace(lib.mc_checksum32_workspace(kind, nchunks, nbytes), src)
+        check(lib.mc_checksum32_batch(kind, src.data_ptr(), src_stride, nchunks, nbytes, init & 0xFFFFFFFF,
+                                      pre.data_ptr() if pre is not None else None,
+                                      pre.numel() if pre is not None else 0,
+                                      out.data_ptr(), ws.data_ptr(), ws.numel(), stream(src)),
+              "mc_checksum32_batch")
+    return out[:nchunks]
+
+
+def checksum32_encode(kind, src, src_stride, dst, dst_stride, nchunks, nbytes, init, location,
+                      prefix=None) -> None:
+    """Checksum32.encode of `nchunks` rows into dst rows (LE32 footer at the start or end)."""
+    _native.require_device()
+    with _guard(src):
+        pre = _prefix_dev(prefix, src)
+        ws = workspace(lib.mc_checksum32_workspace(kind, nchunks, nbytes), src)
+        check(lib.mc_checksum32_encode_batch(kind, src.data_ptr(), src_stride, dst.data_ptr(), dst_stride,
+                                             nchunks, nbytes, init & 0xFFFFFFFF,
+                                             pre.data_ptr() if pre is not None else None,
+                                             pre.numel() if pre is not None else 0, location, None,
+                                             ws.data_ptr(), ws.numel(), stream(src)),
+              "mc_checksum32_encode_batch")
+
+
+def packbits(src, dst, n) -> None:
+    _native.require_device()
+    with _guard(dst):
+        check(lib.mc_packbits(src.data_ptr() if n else None, dst.data_ptr(), n, stream(dst)), "mc_packbits")
+
+
+def unpackbits(src, src_bytes, dst, n) -> None:
+    _native.require_device()
+    if n == 0:
+        return
+    with _guard(src):
+        check(lib.mc_unpackbits(src.data_ptr(), src_bytes, dst.data_ptr(), n, stream(src)), "mc_unpackbits")

@@ -1,0 +1,76 @@
+"""AsType filter (reference: src/numcodecs/astype.py:7-72).
+
+encode: ``ensure_ndarray(buf).view(decode_dtype).astype(encode_dtype)``;
+decode: ``view(encode_dtype).astype(decode_dtype)`` copied into `out` when
+given.  The cast runs on the GPU with numpy's ``astype`` semantics
+(csrc/mc_elementwise.hip ``mc_cast``: wrap-around integer narrowing,
+correctly rounded float narrowing, x86-64 results for out-of-range
+float -> int); shapes follow numpy's ``view`` rule.
+"""
+
+import numpy as np
+
+from . import _ops
+from .abc import Codec
+from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
+from .quantize import _view_shape
+
+__all__ = ["AsType"]
+
+
+def _cast(buf, from_dt, to_dt):
+    src = to_dbuf(buf, flatten=False, contiguous=False)
+    if src.nbytes % from_dt.itemsize:
+        raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
+    n = src.nbytes // from_dt.itemsize
+    shape = _view_shape(src.shape, src.dtype.itemsize, from_dt.itemsize, src.order)
+    dst = empty_like_bytes(n * to_dt.itemsize, src)
+    if from_dt == to_dt:
+        dst.copy_(src.data)
+    else:
+        _ops.cast(src.data, dst, n, from_dt, to_dt)
+    return finish(dst, to_dt, shape, src.order, src.host)
+
+
+class AsType(Codec):
+    """Filter to convert data between different types.
+
+    Parameters
+    ----------
+    encode_dtype : dtype
+        Data type to use for encoded data.
+    decode_dtype : dtype, optional
+        Data type to use for decoded data.
+
+    Notes
+    -----
+    If `encode_dtype` is of lower precision than `decode_dtype`, please be
+    aware that data loss can occur by writing data to disk using this filter.
+    No checks are made to ensure the casting will work in that direction and
+    data corruption will occur.
+    """
+
+    codec_id = "astype"
+
+    def __init__(self, encode_dtype, decode_dtype):
+        self.encode_dtype = np.dtype(encode_dtype)
+        self.decode_dtype = np.dtype(decode_dtype)
+
+    def encode(self, buf):
+        return _cast(buf, self.decode_dtype, self.encode_dtype)
+
+    def decode(self, buf, out=None):
+        return ndarray_copy(_cast(buf, self.encode_dtype, self.decode_dtype), out)
+
+    def get_config(self):
+        return {
+            "id": self.codec_id,
+            "encode_dtype": self.encode_dtype.str,
+            "decode_dtype": self.decode_dtype.str,
+        }
+
+    def __repr__(self):
+        return (
+            f"{type(self).__name__}(encode_dtype={self.encode_dtype.str!r}, "
+            f"decode_dtype={self.decode_dtype.str!r})"
+        )

@@ -40,7 +40,16 @@ __all__ = [
     "fletcher32_unshuffle_decode_chunks",
     "encoded_stride",
     "host_pipeline",
+    "checksum32_chunks",
+    "checksum32_encode_chunks",
 ]
+
+_CK_KINDS = {
+    "crc32": (_native.MC_CK_CRC32, 0),
+    "crc32c": (_native.MC_CK_CRC32C, 0),
+    "adler32": (_native.MC_CK_ADLER32, 1),
+    "jenkins_lookup3": (_native.MC_CK_JENKINS, 0),
+}
 
 
 def _as_rows(chunks: torch.Tensor) -> torch.Tensor:
@@ -50,7 +59,7 @@ def _as_rows(chunks: torch.Tensor) -> torch.Tensor:
     if chunks.dim() < 1:
         raise ValueError("expected a batch dimension")
     b = chunks.shape[0]
-    rows = chunks.reshape(b, -1)
+    rows = chunks.reshape(b, -1) if chunks.numel() else chunks.reshape(b, 0)
     if rows.stride(1) != 1:
         raise ValueError("each chunk must be contiguous")
     rows = rows.view(torch.uint8) if rows.element_size() != 1 or rows.dtype != torch.uint8 else rows
@@ -97,6 +106,42 @@ def fletcher32_chunks(chunks, nbytes=None) -> torch.Tensor:
                                           ws.data_ptr(), ws.numel(), _ops.stream(rows)),
                   "mc_fletcher32_batch")
     return res.to(torch.int64) & 0xFFFFFFFF
+
+
+def checksum32_chunks(chunks, codec_id, nbytes=None, value=None, prefix=None) -> torch.Tensor:
+    """`codec_id` checksum ('crc32', 'crc32c', 'adler32', 'jenkins_lookup3')
+    of every chunk (first `nbytes` of each row), one launch; int64 [B].
+    `value` defaults to the codec's own seed (0, or 1 for adler32); `prefix`
+    (jenkins_lookup3 only) is hashed before every chunk."""
+    kind, default = _CK_KINDS[codec_id]
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    nbytes = n if nbytes is None else nbytes
+    if b == 0:
+        return torch.empty(0, dtype=torch.int64, device=rows.device)
+    res = _ops.checksum32(kind, rows, rows.stride(0), b, nbytes, default if value is None else value, prefix)
+    return res.to(torch.int64) & 0xFFFFFFFF
+
+
+def checksum32_encode_chunks(chunks, codec_id, location=None, out=None, value=None, prefix=None):
+    """Checksum32.encode of every chunk in one launch: rows of
+    ``chunk_bytes + 4`` (checksum at the codec's default location, or
+    `location`).  Returns the [B, chunk_bytes + 4] uint8 batch (or `out`)."""
+    kind, default = _CK_KINDS[codec_id]
+    if location is None:
+        location = "end" if codec_id in ("crc32c", "jenkins_lookup3") else "start"
+    if location not in ("start", "end") or (codec_id == "jenkins_lookup3" and location != "end"):
+        raise ValueError(f"Invalid checksum location: {location}")
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    out = torch.empty((b, n + 4), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if out.shape[1] < n + 4:
+        raise ValueError("output rows must hold chunk_bytes + 4 bytes")
+    if b:
+        loc = _native.MC_CK_START if location == "start" else _native.MC_CK_END
+        _ops.checksum32_encode(kind, rows, rows.stride(0), out, out.stride(0), b, n,
+                               default if value is None else value, loc, prefix)
+    return out
 
 
 def shuffle_fletcher32_encode_chunks(chunks, elementsize, out=None):

@@ -1,0 +1,585 @@
+// mc_checksum.hip -- the Checksum32 family (checksum32.py:45-209): CRC32
+// (zlib.crc32), CRC32C (crc32c / google_crc32c), Adler32 (zlib.adler32) and
+// JenkinsLookup3 (jenkins.pyx:93-325), one checksum per chunk over batches of
+// chunks, optionally fused with the payload copy of Checksum32.encode.
+//
+// CRC32 / CRC32C (reflected polynomials 0xEDB88320 / 0x82F63B78).  With the
+// raw register update raw(c, D) (no pre/post inversion) the CRC is linear over
+// GF(2):  raw(c, D) = c * x^(8|D|) xor raw(0, D)  and  raw(0, zeros ++ D) =
+// raw(0, D), and zlib's crc32(D, value) = ~raw(~value, D).  A workgroup owns a
+// tile of K * 4096 bytes; lane l reads the 16-B vectors at l*16 + k*4096
+// (every load instruction of the wave covers 1 KiB contiguously) and runs
+//     acc = raw(acc, v ++ zeros(4080))
+// with one slicing-by-16 lookup set whose 16 tables already include the
+// 4080-byte shift (V[m][b] = raw(0, byte b ++ zeros(15 - m + 4080))): 16 LDS
+// lookups per 16 bytes.  Lane l's accumulator then stands 16*l bytes past the
+// tile end; multiplying by x^(-128 l) (x is invertible mod P) aligns every
+// lane, and the lanes' values XOR together into the tile's raw CRC.  A
+// per-chunk finalize combines tiles with Horner steps by x^(8 * tile bytes)
+// and undoes the zero padding of the last tile with x^(-8 * pad).  Bytes past
+// the chunk end are read as zeros, so all loads stay vector loads.
+//
+// Adler32: a = a0 + S1, b = b0 + n*a0 + S2 (mod 65521) with S1 = sum d_i and
+// S2 = sum (n - i) d_i -- absolute weights, so it is a plain parallel
+// reduction exactly like Fletcher32 (mc_fletcher.hip); byte sums per dword
+// come from v_dot4_u32_u8.
+//
+// JenkinsLookup3 (Bob Jenkins' hashlittle as restated by HDF5) is a serial
+// chain of 12-byte mixing rounds with no algebraic shortcut: one thread per
+// chunk, so a batch of chunks runs in parallel and a single chunk runs at
+// single-thread speed (documented in DESIGN.md).
+#include "mc_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// GF(2)[x] mod P in the reflected representation (bit 31 = x^0, bit 0 = x^31)
+// ---------------------------------------------------------------------------
+constexpr uint32_t POLY_CRC32 = 0xEDB88320u;
+constexpr uint32_t POLY_CRC32C = 0x82F63B78u;
+constexpr uint32_t GF_ONE = 0x80000000u;  // x^0
+constexpr uint32_t GF_X = 0x40000000u;    // x^1
+
+constexpr MC_HD uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & (GF_ONE >> i)) p ^= b;                   // + a_i * b * x^i
+    b = (b & 1u) ? ((b >> 1) ^ poly) : (b >> 1);     // b *= x
+  }
+  return p;
+}
+
+constexpr int STEP = MC_BLOCK * 16;  // bytes between a lane's consecutive vectors
+constexpr int SHIFT = STEP - 16;     // zero bytes folded into the tables
+
+struct CrcConsts {
+  uint32_t v[16][256];  // V[m][b] = raw(0, byte b ++ zeros(15 - m + SHIFT))
+  uint32_t g[MC_BLOCK];  // x^(-128 l): moves lane l's accumulator back 16*l bytes
+  uint32_t x2n[64];      // x^(2^k)
+  uint32_t x2n_inv[64];  // x^(-2^k)
+};
+
+constexpr uint32_t xpow_tab(const uint32_t (&tab)[64], uint64_t e, uint32_t poly) {
+  uint32_t p = GF_ONE;
+  for (int k = 0; e; ++k, e >>= 1)
+    if (e & 1) p = gf_mul(p, tab[k], poly);
+  return p;
+}
+
+constexpr CrcConsts make_crc_consts(uint32_t poly) {
+  CrcConsts c{};
+  uint32_t t[16][256] = {};
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t r = b;
+    for (int k = 0; k < 8; ++k) r = (r & 1u) ? ((r >> 1) ^ poly) : (r >> 1);
+    t[0][b] = r;  // raw(0, byte b)
+  }
+  for (int k = 1; k < 16; ++k)
+    for (int b = 0; b < 256; ++b) t[k][b] = (t[k - 1][b] >> 8) ^ t[0][t[k - 1][b] & 0xffu];
+  c.x2n[0] = GF_X;
+  for (int k = 1; k < 64; ++k) c.x2n[k] = gf_mul(c.x2n[k - 1], c.x2n[k - 1], poly);
+  // x * (P(x) - 1)/x = P(x) - 1 = 1 (mod P, mod 2): x^-1 = (P - 1)/x
+  c.x2n_inv[0] = (poly << 1) | 1u;
+  for (int k = 1; k < 64; ++k) c.x2n_inv[k] = gf_mul(c.x2n_inv[k - 1], c.x2n_inv[k - 1], poly);
+  const uint32_t z = xpow_tab(c.x2n, 8ull * SHIFT, poly);
+  for (int m = 0; m < 16; ++m) {
+    uint32_t basis[8] = {};
+    for (int j = 0; j < 8; ++j) basis[j] = gf_mul(t[15 - m][1u << j], z, poly);
+    for (int b = 0; b < 256; ++b) {  // raw(0, .) is linear in the byte
+      uint32_t r = 0;
+      for (int j = 0; j < 8; ++j)
+        if (b & (1 << j)) r ^= basis[j];
+      c.v[m][b] = r;
+    }
+  }
+  c.g[0] = GF_ONE;
+  for (int l = 1; l < MC_BLOCK; ++l) c.g[l] = gf_mul(c.g[l - 1], c.x2n_inv[7], poly);
+  return c;
+}
+
+static_assert(gf_mul(GF_X, (POLY_CRC32 << 1) | 1u, POLY_CRC32) == GF_ONE, "x^-1 (CRC32)");
+static_assert(gf_mul(GF_X, (POLY_CRC32C << 1) | 1u, POLY_CRC32C) == GF_ONE, "x^-1 (CRC32C)");
+
+__constant__ const CrcConsts kCrc32 = make_crc_consts(POLY_CRC32);
+__constant__ const CrcConsts kCrc32c = make_crc_consts(POLY_CRC32C);
+
+enum Kind { K_CRC32 = MC_CK_CRC32, K_CRC32C = MC_CK_CRC32C, K_ADLER = MC_CK_ADLER32 };
+
+template <int KIND>
+MC_DEV const CrcConsts &crc_consts() {
+  if constexpr (KIND == K_CRC32C) return kCrc32c;
+  else return kCrc32;
+}
+template <int KIND>
+constexpr uint32_t crc_poly() { return KIND == K_CRC32C ? POLY_CRC32C : POLY_CRC32; }
+
+template <int KIND>
+MC_DEV uint32_t xpow(const uint32_t *tab, uint64_t e) {
+  uint32_t p = GF_ONE;
+  for (int k = 0; e; ++k, e >>= 1)
+    if (e & 1) p = gf_mul(p, tab[k], crc_poly<KIND>());
+  return p;
+}
+
+// acc = raw(acc, v ++ zeros(SHIFT)) with the 16 LDS tables
+MC_DEV uint32_t slice16(const uint32_t *__restrict__ V, uint32_t acc, mc_u32x4 v) {
+  const uint32_t d = acc ^ v.x;
+  return V[0 * 256 + (d & 0xffu)] ^ V[1 * 256 + ((d >> 8) & 0xffu)] ^
+         V[2 * 256 + ((d >> 16) & 0xffu)] ^ V[3 * 256 + (d >> 24)] ^
+         V[4 * 256 + (v.y & 0xffu)] ^ V[5 * 256 + ((v.y >> 8) & 0xffu)] ^
+         V[6 * 256 + ((v.y >> 16) & 0xffu)] ^ V[7 * 256 + (v.y >> 24)] ^
+         V[8 * 256 + (v.z & 0xffu)] ^ V[9 * 256 + ((v.z >> 8) & 0xffu)] ^
+         V[10 * 256 + ((v.z >> 16) & 0xffu)] ^ V[11 * 256 + (v.z >> 24)] ^
+         V[12 * 256 + (v.w & 0xffu)] ^ V[13 * 256 + ((v.w >> 8) & 0xffu)] ^
+         V[14 * 256 + ((v.w >> 16) & 0xffu)] ^ V[15 * 256 + (v.w >> 24)];
+}
+
+// ---------------------------------------------------------------------------
+// 16-B accesses at byte position pos of a chunk of n bytes; bytes >= n read
+// as 0 and are not written.  AL: 2 = 16-B aligned (nontemporal), 1 = 4-B
+// aligned (global_load/store_dwordx4 at dword alignment), 0 = bytes.
+// ---------------------------------------------------------------------------
+template <int AL>
+MC_DEV mc_u32x4 ld_vec(const uint8_t *p) {
+  if constexpr (AL == 2) {
+    return mc_ld16<true>(p);
+  } else if constexpr (AL == 1) {
+    mc_u32x4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
+    return v;
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)p[4 * j] | ((uint32_t)p[4 * j + 1] << 8) | ((uint32_t)p[4 * j + 2] << 16) |
+             ((uint32_t)p[4 * j + 3] << 24);
+    return mc_u32x4{w[0], w[1], w[2], w[3]};
+  }
+}
+template <int AL>
+MC_DEV void st_vec(uint8_t *p, mc_u32x4 v) {
+  if constexpr (AL == 2) {
+    mc_st16<true>(p, v);
+  } else if constexpr (AL == 1) {
+    __builtin_memcpy(__builtin_assume_aligned(p, 4), &v, 16);
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) p[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+  }
+}
+template <int AL>
+MC_DEV mc_u32x4 ld_masked(const uint8_t *s, size_t pos, size_t n) {
+  if (pos + 16 <= n) return ld_vec<AL>(s + pos);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 16; ++j)
+    if (pos + j < n) w[j >> 2] |= (uint32_t)s[pos + j] << (8 * (j & 3));
+  return mc_u32x4{w[0], w[1], w[2], w[3]};
+}
+template <int AL>
+MC_DEV void st_masked(uint8_t *d, size_t pos, size_t n, mc_u32x4 v) {
+  if (pos + 16 <= n) {
+    st_vec<AL>(d + pos, v);
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (int j = 0; j < 16; ++j)
+    if (pos + j < n) d[pos + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+}
+
+constexpr uint32_t ADLER_P = 65521u;
+
+MC_DEV uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+  return v;
+}
+MC_DEV uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Per-tile partials.  Block loops over tiles (tile = chunk * tiles_per_chunk
+// + t); the CRC tables are staged into LDS once per block.
+//   CRC:   partials[tile] = raw(0, tile bytes ++ zero padding to K*STEP)
+//   Adler: partials[2*tile] = S1 mod P, partials[2*tile+1] = S2 mod P
+// COPY: also write the payload to dst (+ per-row offset already applied).
+// ---------------------------------------------------------------------------
+template <int KIND, int K, bool COPY, int ALS, int ALD>
+__global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
+    const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
+    size_t dst_stride, size_t n, size_t tiles_per_chunk, size_t total_tiles,
+    uint32_t *__restrict__ partials) {
+  constexpr bool CRC = KIND != K_ADLER;
+  __shared__ uint32_t V[CRC ? 16 * 256 : 1];
+  __shared__ uint64_t red[2][MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t g = 0;
+  if constexpr (CRC) {
+    const mc_u32x4 *tv = reinterpret_cast<const mc_u32x4 *>(&crc_consts<KIND>().v[0][0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      reinterpret_cast<mc_u32x4 *>(V)[threadIdx.x + i * MC_BLOCK] = tv[threadIdx.x + i * MC_BLOCK];
+    g = crc_consts<KIND>().g[threadIdx.x];
+    __syncthreads();
+  }
+  for (size_t tile = blockIdx.x; tile < total_tiles; tile += gridDim.x) {
+    const size_t c = tile / tiles_per_chunk;
+    const size_t t = tile - c * tiles_per_chunk;
+    const uint8_t *s = src + c * src_stride;
+    const size_t base = t * (size_t)(K * STEP) + 16 * (size_t)threadIdx.x;
+    mc_u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const size_t pos = base + (size_t)k * STEP;
+      v[k] = pos < n ? ld_masked<ALS>(s, pos, n) : mc_u32x4{0, 0, 0, 0};
+    }
+    if constexpr (COPY) {
+      uint8_t *d = dst + c * dst_stride;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const size_t pos = base + (size_t)k * STEP;
+        if (pos < n) st_masked<ALD>(d, pos, n, v[k]);
+      }
+    }
+    if constexpr (CRC) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = slice16(V, acc, v[k]);
+      acc = wave_xor(gf_mul(acc, g, crc_poly<KIND>()));
+      if (lane == 0) red[0][wave] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t r = 0;
+        for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
+        partials[tile] = r;
+      }
+    } else {
+      uint64_t s1 = 0, s2a = 0, s2b = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const size_t pos = base + (size_t)k * STEP;
+        const mc_u32x4 x = v[k];
+        const uint32_t a0 = __builtin_amdgcn_udot4(x.x, 0x01010101u, 0u, false);
+        const uint32_t a1 = __builtin_amdgcn_udot4(x.y, 0x01010101u, 0u, false);
+        const uint32_t a2 = __builtin_amdgcn_udot4(x.z, 0x01010101u, 0u, false);
+        const uint32_t a3 = __builtin_amdgcn_udot4(x.w, 0x01010101u, 0u, false);
+        uint32_t b = __builtin_amdgcn_udot4(x.x, 0x03020100u, 0u, false);
+        b = __builtin_amdgcn_udot4(x.y, 0x07060504u, b, false);
+        b = __builtin_amdgcn_udot4(x.z, 0x0b0a0908u, b, false);
+        b = __builtin_amdgcn_udot4(x.w, 0x0f0e0d0cu, b, false);
+        const uint32_t a = a0 + a1 + a2 + a3;
+        // weight of the vector's first byte: n - pos (mod P); bytes >= n are 0
+        const uint32_t cw = pos < n ? (uint32_t)((n - pos) % ADLER_P) + ADLER_P : 0u;
+        s1 += a;
+        s2a += (uint64_t)cw * a;
+        s2b += b;
+      }
+      const uint64_t r1 = wave_sum(s1 % ADLER_P);
+      const uint64_t r2 = wave_sum((s2a % ADLER_P + ADLER_P - s2b % ADLER_P) % ADLER_P);
+      if (lane == 0) {
+        red[0][wave] = r1;
+        red[1][wave] = r2;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint64_t x = 0, y = 0;
+        for (int w = 0; w < MC_BLOCK / 64; ++w) {
+          x += red[0][w];
+          y += red[1][w];
+        }
+        partials[2 * tile] = (uint32_t)(x % ADLER_P);
+        partials[2 * tile + 1] = (uint32_t)(y % ADLER_P);
+      }
+    }
+    __syncthreads();  // red[] is reused by the next tile
+  }
+}
+
+MC_DEV void store_le32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+  p[3] = (uint8_t)(v >> 24);
+}
+
+// One block per chunk: fold the tile partials into the checksum; write it to
+// out[c] (if out) and/or as a little-endian footer at footer + c*footer_stride.
+template <int KIND, int K>
+__global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
+    const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
+    uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride) {
+  __shared__ uint64_t red[2][MC_BLOCK / 64];
+  const size_t c = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t lo = tiles_per_chunk * threadIdx.x / MC_BLOCK;
+  const size_t hi = tiles_per_chunk * (threadIdx.x + 1) / MC_BLOCK;
+  uint32_t result;
+  if constexpr (KIND == K_ADLER) {
+    uint64_t s1 = 0, s2 = 0;
+    for (size_t j = lo; j < hi; ++j) {
+      s1 += partials[2 * (c * tiles_per_chunk + j)];
+      s2 += partials[2 * (c * tiles_per_chunk + j) + 1];
+    }
+    s1 = wave_sum(s1 % ADLER_P);
+    s2 = wave_sum(s2 % ADLER_P);
+    if (lane == 0) {
+      red[0][wave] = s1;
+      red[1][wave] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint64_t x = 0, y = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) {
+      x += red[0][w];
+      y += red[1][w];
+    }
+    // zlib.adler32(data, value): a0 = value & 0xffff, b0 = value >> 16
+    const uint64_t a0 = init & 0xffffu, b0 = init >> 16;
+    const uint64_t a = (a0 + x) % ADLER_P;
+    const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
+    result = (uint32_t)((b << 16) | a);
+  } else {
+    const CrcConsts &C = crc_consts<KIND>();
+    constexpr uint64_t TB = (uint64_t)K * STEP;
+    const uint32_t X = xpow<KIND>(C.x2n, 8 * TB);
+    uint32_t acc = 0;
+    for (size_t j = lo; j < hi; ++j)
+      acc = gf_mul(acc, X, crc_poly<KIND>()) ^ partials[c * tiles_per_chunk + j];
+    if (hi > lo) acc = gf_mul(acc, xpow<KIND>(C.x2n, 8 * TB * (tiles_per_chunk - hi)), crc_poly<KIND>());
+    acc = wave_xor(acc);
+    if (lane == 0) red[0][wave] = acc;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint32_t r = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
+    // r covers tiles_per_chunk * TB bytes; the last (TB*tiles - n) are padding
+    r = gf_mul(r, xpow<KIND>(C.x2n_inv, 8 * (TB * tiles_per_chunk - n)), crc_poly<KIND>());
+    // crc(D, value) = ~raw(~value, D) = ~(~value * x^(8n) xor raw(0, D))
+    result = ~(gf_mul(~init, xpow<KIND>(C.x2n, 8 * (uint64_t)n), crc_poly<KIND>()) ^ r);
+  }
+  if (out) out[c] = result;
+  if (footer) store_le32(footer + c * footer_stride, result);
+}
+
+// ---------------------------------------------------------------------------
+// JenkinsLookup3 (jenkins.pyx:93-325): one thread per chunk over the virtual
+// stream prefix ++ chunk.
+// ---------------------------------------------------------------------------
+MC_DEV uint32_t jrot(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+MC_DEV void jmix(uint32_t &a, uint32_t &b, uint32_t &c) {  // jenkins.pyx:264-325
+  a -= c; a ^= jrot(c, 4);  c += b;
+  b -= a; b ^= jrot(a, 6);  a += c;
+  c -= b; c ^= jrot(b, 8);  b += a;
+  a -= c; a ^= jrot(c, 16); c += b;
+  b -= a; b ^= jrot(a, 19); a += c;
+  c -= b; c ^= jrot(b, 4);  b += a;
+}
+
+MC_DEV uint32_t jfinal(uint32_t a, uint32_t b, uint32_t c) {  // jenkins.pyx:221-259
+  c ^= b; c -= jrot(b, 14);
+  a ^= c; a -= jrot(c, 11);
+  b ^= a; b -= jrot(a, 25);
+  c ^= b; c -= jrot(b, 16);
+  a ^= c; a -= jrot(c, 4);
+  b ^= a; b -= jrot(a, 14);
+  c ^= b; c -= jrot(b, 24);
+  return c;
+}
+
+MC_DEV uint32_t jbyte(const uint8_t *pre, size_t plen, const uint8_t *s, size_t i) {
+  return i < plen ? pre[i] : s[i - plen];
+}
+
+__global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src, size_t src_stride,
+                                                size_t nchunks, size_t n, uint32_t init,
+                                                const uint8_t *__restrict__ prefix, size_t plen,
+                                                uint32_t *__restrict__ out,
+                                                uint8_t *__restrict__ footer,
+                                                size_t footer_stride) {
+  const size_t ci = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= nchunks) return;
+  const uint8_t *s = src + ci * src_stride;
+  const size_t L = plen + n;
+  uint32_t a, b, c;
+  a = b = c = 0xdeadbeefu + (uint32_t)L + init;
+  if (L > 0) {
+    const size_t nb = (L - 1) / 12;  // full mixing blocks ("while length > 12")
+    size_t blk = 0;
+    if (plen == 0 && ((uintptr_t)s & 3) == 0) {
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s);
+      for (; blk + 4 <= nb; blk += 4) {
+        uint32_t q[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) q[j] = w[3 * blk + j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a += q[3 * r];
+          b += q[3 * r + 1];
+          c += q[3 * r + 2];
+          jmix(a, b, c);
+        }
+      }
+      for (; blk < nb; ++blk) {
+        a += w[3 * blk];
+        b += w[3 * blk + 1];
+        c += w[3 * blk + 2];
+        jmix(a, b, c);
+      }
+    } else {
+      for (; blk < nb; ++blk) {
+        uint32_t q[3] = {0, 0, 0};
+        for (int j = 0; j < 12; ++j) q[j >> 2] += jbyte(prefix, plen, s, 12 * blk + j) << (8 * (j & 3));
+        a += q[0];
+        b += q[1];
+        c += q[2];
+        jmix(a, b, c);
+      }
+    }
+    // last block: 1..12 bytes (the fall-through switch of jenkins.pyx:167-214)
+    const size_t r = L - 12 * nb;
+    uint32_t q[3] = {0, 0, 0};
+    for (size_t j = 0; j < r; ++j) q[j >> 2] += jbyte(prefix, plen, s, 12 * nb + j) << (8 * (j & 3));
+    a += q[0];
+    b += q[1];
+    c += q[2];
+    c = jfinal(a, b, c);
+  }
+  if (out) out[ci] = c;
+  if (footer) store_le32(footer + ci * footer_stride, c);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+constexpr unsigned CK_MAX_GRID = 2048;
+
+// tile size (in STEP units) for a chunk: K = 1 below 64 KiB, else 16
+inline int ck_k(size_t n) { return n < (size_t)16 * STEP ? 1 : 16; }
+inline size_t ck_tiles(size_t n, int K) {
+  const size_t tb = (size_t)K * STEP;
+  return n ? (n + tb - 1) / tb : 1;
+}
+inline int align_class(const void *p, size_t stride, size_t nchunks) {
+  const uintptr_t a = (uintptr_t)p | (nchunks > 1 ? stride : 0);
+  return (a & 15) == 0 ? 2 : (a & 3) == 0 ? 1 : 0;
+}
+
+template <int KIND, int K, bool COPY, int ALS, int ALD>
+void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
+                  size_t total, uint32_t *parts, hipStream_t st) {
+  const unsigned grid = (unsigned)(total < CK_MAX_GRID ? total : CK_MAX_GRID);
+  k_ck_tiles<KIND, K, COPY, ALS, ALD><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts);
+}
+
+template <int KIND, int K>
+void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
+                    size_t tpc, uint32_t *parts, hipStream_t st) {
+  const size_t total = tpc * nchunks;
+  const int als = align_class(s, ss, nchunks);
+  if (!d) {
+    if (als == 2) launch_tiles<KIND, K, false, 2, 2>(s, ss, d, ds, n, tpc, total, parts, st);
+    else if (als == 1) launch_tiles<KIND, K, false, 1, 1>(s, ss, d, ds, n, tpc, total, parts, st);
+    else launch_tiles<KIND, K, false, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
+    return;
+  }
+  const int ald = align_class(d, ds, nchunks);
+  if (als == 2 && ald == 2) launch_tiles<KIND, K, true, 2, 2>(s, ss, d, ds, n, tpc, total, parts, st);
+  else if (als == 2 && ald == 1) launch_tiles<KIND, K, true, 2, 1>(s, ss, d, ds, n, tpc, total, parts, st);
+  else if (als >= 1 && ald >= 1) launch_tiles<KIND, K, true, 1, 1>(s, ss, d, ds, n, tpc, total, parts, st);
+  else launch_tiles<KIND, K, true, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
+}
+
+template <int KIND>
+int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
+                  uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, void *ws,
+                  size_t ws_bytes, hipStream_t st) {
+  const int K = ck_k(n);
+  const size_t tpc = ck_tiles(n, K);
+  const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
+  if (!ws || ws_bytes < need) return MC_ENOSPC;
+  uint32_t *parts = static_cast<uint32_t *>(ws);
+  if (K == 1) {
+    dispatch_tiles<KIND, 1>(s, ss, d, ds, nchunks, n, tpc, parts, st);
+    k_ck_finalize<KIND, 1><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out, footer, fs);
+  } else {
+    dispatch_tiles<KIND, 16>(s, ss, d, ds, nchunks, n, tpc, parts, st);
+    k_ck_finalize<KIND, 16><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out, footer, fs);
+  }
+  return mc_last_launch();
+}
+
+int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks,
+                size_t n, uint32_t init, const uint8_t *prefix, size_t plen, uint32_t *out,
+                uint8_t *footer, size_t fs, void *ws, size_t ws_bytes, hipStream_t st) {
+  switch (kind) {
+    case MC_CK_CRC32:
+      return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+    case MC_CK_CRC32C:
+      return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+    case MC_CK_ADLER32:
+      return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+    case MC_CK_JENKINS: {
+      if (d && n) {
+        const hipError_t e = hipMemcpy2DAsync(d, ds, s, ss, n, nchunks, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return mc_hip_status(e);
+      }
+      const unsigned grid = (unsigned)((nchunks + 63) / 64);
+      k_jenkins<<<grid, 64, 0, st>>>(s, ss, nchunks, n, init, prefix, plen, out, footer, fs);
+      return mc_last_launch();
+    }
+    default:
+      return MC_EINVAL;
+  }
+}
+
+bool valid_kind(int kind) { return kind >= MC_CK_CRC32 && kind <= MC_CK_JENKINS; }
+
+}  // namespace
+
+extern "C" {
+
+size_t mc_checksum32_workspace(int kind, size_t nchunks, size_t chunk_bytes) {
+  if (!valid_kind(kind) || kind == MC_CK_JENKINS) return 0;
+  const size_t tpc = ck_tiles(chunk_bytes, ck_k(chunk_bytes));
+  return tpc * nchunks * (kind == MC_CK_ADLER32 ? 8 : 4);
+}
+
+int mc_checksum32_batch(int kind, const void *src, size_t src_stride, size_t nchunks,
+                        size_t chunk_bytes, uint32_t init, const void *prefix, size_t prefix_bytes,
+                        uint32_t *out_sums, void *workspace, size_t workspace_bytes,
+                        mc_stream_t stream) {
+  if (!valid_kind(kind)) return MC_EINVAL;
+  if (nchunks == 0) return MC_OK;
+  if (!out_sums || (chunk_bytes && !src) || (nchunks > 1 && src_stride < chunk_bytes)) return MC_EINVAL;
+  if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
+  if (nchunks > 0x7fffffffu) return MC_EINVAL;
+  return ck_dispatch(kind, static_cast<const uint8_t *>(src), src_stride, nullptr, 0, nchunks,
+                     chunk_bytes, init, static_cast<const uint8_t *>(prefix), prefix_bytes,
+                     out_sums, nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int mc_checksum32_encode_batch(int kind, const void *src, size_t src_stride, void *dst,
+                               size_t dst_stride, size_t nchunks, size_t chunk_bytes,
+                               uint32_t init, const void *prefix, size_t prefix_bytes,
+                               int location, uint32_t *out_sums, void *workspace,
+                               size_t workspace_bytes, mc_stream_t stream) {
+  if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
+  if (nchunks == 0) return MC_OK;
+  if (!dst || (chunk_bytes && !src)) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < chunk_bytes || dst_stride < chunk_bytes + 4)) return MC_EINVAL;
+  if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
+  if (nchunks > 0x7fffffffu) return MC_EINVAL;
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  uint8_t *payload = location == MC_CK_START ? d + 4 : d;
+  uint8_t *footer = location == MC_CK_START ? d : d + chunk_bytes;
+  return ck_dispatch(kind, static_cast<const uint8_t *>(src), src_stride, payload, dst_stride,
+                     nchunks, chunk_bytes, init, static_cast<const uint8_t *>(prefix),
+                     prefix_bytes, out_sums, footer, dst_stride, workspace, workspace_bytes,
+                     (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,50 @@
+"""PackBits filter (reference: src/numcodecs/packbits.py:7-82).
+
+encode: booleans -> ``[n_bits_padded] ++ np.packbits(arr)`` (MSB first);
+decode: ``np.unpackbits`` minus the padding, as a bool array (copied into
+`out` when given).  Both directions are one GPU pass (csrc/mc_bits.hip).
+"""
+
+import numpy as np
+import torch
+
+from . import _ops
+from .abc import Codec
+from .compat import download, empty_like_bytes, finish, ndarray_copy, to_dbuf
+
+__all__ = ["PackBits"]
+
+
+class PackBits(Codec):
+    """Codec to pack elements of a boolean array into bits in a uint8 array.
+
+    Notes
+    -----
+    The first element of the encoded array stores the number of bits that
+    were padded to complete the final byte.
+    """
+
+    codec_id = "packbits"
+
+    def encode(self, buf):
+        # ensure_ndarray(buf).view(bool).reshape(-1, order='A')
+        src = to_dbuf(buf, flatten=True, contiguous=False)
+        n = src.nbytes  # one bool per byte
+        dst = empty_like_bytes(1 + (n + 7) // 8, src)
+        _ops.packbits(src.data, dst, n)
+        return finish(dst, np.dtype("u1"), (dst.numel(),), "C", src.host)
+
+    def decode(self, buf, out=None):
+        src = to_dbuf(buf, flatten=True, contiguous=False)
+        nb = src.nbytes
+        if nb == 0:  # enc[0] of an empty array
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        pad = int(download(src.data[:1])[0])
+        n = max(8 * (nb - 1) - pad, 0)
+        dst = empty_like_bytes(n, src)
+        _ops.unpackbits(src.data, nb, dst, n)
+        if src.host:
+            dec = download(dst).view(bool)
+        else:
+            dec = dst.view(torch.bool)
+        return ndarray_copy(dec, out)

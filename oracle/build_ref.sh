@@ -6,6 +6,7 @@
 #
 #   src/numcodecs/_shuffle.pyx    -> oracle/_ref/_shuffle.*.so   (_doShuffle/_doUnshuffle)
 #   src/numcodecs/fletcher32.pyx  -> oracle/_ref/fletcher32.*.so (+ _utils.pxd)
+#   src/numcodecs/jenkins.pyx     -> oracle/_ref/jenkins.*.so    (jenkins_lookup3)
 #
 # Flags follow the reference's release build (src/numcodecs/meson.build:245-254):
 # plain -O3, no -march, -pthread.  Nothing is written outside oracle/_ref/.
@@ -24,7 +25,7 @@ trap 'rm -rf "$TMP"' EXIT
 PY=${PYTHON:-python3}
 EXT=$($PY -c 'import sysconfig; print(sysconfig.get_config_var("EXT_SUFFIX"))')
 PYINC=$($PY -c 'import sysconfig; print(sysconfig.get_paths()["include"])')
-for mod in _shuffle fletcher32; do
+for mod in _shuffle fletcher32 jenkins; do
   if [ "$OUT/$mod$EXT" -nt "$SRC/$mod.pyx" ] 2>/dev/null; then continue; fi
   # -I $SRC/.. so `from ._utils cimport ...` resolves inside package numcodecs
   $PY -m cython -3 -I "$SRC/.." "$SRC/$mod.pyx" -o "$TMP/$mod.c"

@@ -9,6 +9,12 @@
  *   nco_unshuffle    <- _shuffle.pyx:23-30  _doUnshuffle
  *   nco_fletcher32   <- fletcher32.pyx:24-57 _fletcher32 (HDF5 H5checksum.c
  *                       algorithm: 360-word blocks, big-endian 16-bit words)
+ *   nco_jenkins_lookup3 <- jenkins.pyx:93-325 (hashlittle as in HDF5)
+ *   nco_crc32c       <- checksum32.py:189-209 CRC32C.checksum, which calls the
+ *                       third-party google_crc32c / crc32c package (absent
+ *                       here): CRC-32C (Castagnoli, reflected 0x82F63B78,
+ *                       init/xorout 0xFFFFFFFF), restated bit by bit and pinned
+ *                       by the reference's fixture/crc32c files.
  * Built with plain -O3 and no -march, like the reference's release build
  * (src/numcodecs/meson.build:245-254).
  */
@@ -69,4 +75,49 @@ void nco_unshuffle_batch(const uint8_t *src, uint8_t *des, size_t nchunks, size_
                          size_t element_size) {
   for (size_t c = 0; c < nchunks; c++)
     nco_unshuffle(src + c * chunk_bytes, des + c * chunk_bytes, chunk_bytes, element_size);
+}
+
+/* ---- jenkins.pyx:93-325 ------------------------------------------------ */
+static uint32_t nco_rot(uint32_t x, int k) { return (x << k) ^ (x >> (32 - k)); }
+
+uint32_t nco_jenkins_lookup3(const uint8_t *k, size_t length, uint32_t initval) {
+  uint32_t a, b, c;
+  a = b = c = 0xdeadbeefu + (uint32_t)length + initval;
+  if (length == 0) return c;
+  while (length > 12) {
+    a += k[0] + ((uint32_t)k[1] << 8) + ((uint32_t)k[2] << 16) + ((uint32_t)k[3] << 24);
+    b += k[4] + ((uint32_t)k[5] << 8) + ((uint32_t)k[6] << 16) + ((uint32_t)k[7] << 24);
+    c += k[8] + ((uint32_t)k[9] << 8) + ((uint32_t)k[10] << 16) + ((uint32_t)k[11] << 24);
+    a -= c; a ^= nco_rot(c, 4);  c += b;
+    b -= a; b ^= nco_rot(a, 6);  a += c;
+    c -= b; c ^= nco_rot(b, 8);  b += a;
+    a -= c; a ^= nco_rot(c, 16); c += b;
+    b -= a; b ^= nco_rot(a, 19); a += c;
+    c -= b; c ^= nco_rot(b, 4);  b += a;
+    length -= 12;
+    k += 12;
+  }
+  /* last block: bytes 11..0 of a 1..12-byte tail (the fall-through chain) */
+  for (size_t i = length; i-- > 0;) {
+    const uint32_t v = (uint32_t)k[i] << (8 * (i & 3));
+    if (i >= 8) c += v; else if (i >= 4) b += v; else a += v;
+  }
+  c ^= b; c -= nco_rot(b, 14);
+  a ^= c; a -= nco_rot(c, 11);
+  b ^= a; b -= nco_rot(a, 25);
+  c ^= b; c -= nco_rot(b, 16);
+  a ^= c; a -= nco_rot(c, 4);
+  b ^= a; b -= nco_rot(a, 14);
+  c ^= b; c -= nco_rot(b, 24);
+  return c;
+}
+
+/* ---- CRC-32C, bit by bit ---------------------------------------------- */
+uint32_t nco_crc32c(const uint8_t *p, size_t n, uint32_t value) {
+  uint32_t c = ~value;
+  for (size_t i = 0; i < n; i++) {
+    c ^= p[i];
+    for (int j = 0; j < 8; j++) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+  }
+  return ~c;
 }

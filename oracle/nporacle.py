@@ -33,6 +33,10 @@ def _c():
         lib.nco_unshuffle_batch.argtypes = [vp, vp, sz, sz, sz]
         lib.nco_fletcher32.argtypes = [vp, sz]
         lib.nco_fletcher32.restype = ctypes.c_uint32
+        lib.nco_jenkins_lookup3.argtypes = [vp, sz, ctypes.c_uint32]
+        lib.nco_jenkins_lookup3.restype = ctypes.c_uint32
+        lib.nco_crc32c.argtypes = [vp, sz, ctypes.c_uint32]
+        lib.nco_crc32c.restype = ctypes.c_uint32
         _lib = lib
     return _lib
 
@@ -217,6 +221,94 @@ def fso_decode(buf, offset, scale, dtype, astype=None) -> np.ndarray:
     enc = np.asarray(buf).view(astype).reshape(-1, order="A")
     dec = (enc / scale) + offset
     return dec.astype(dtype, copy=False)
+
+
+# --------------------------------------------------------------------------
+# Checksum32 family: checksum32.py:45-209, jenkins.pyx:93-325
+# --------------------------------------------------------------------------
+def crc32(buf, value: int = 0) -> int:
+    """CRC32.checksum (checksum32.py:106-111) = zlib.crc32 -- the reference's
+    own dependency (CPython's zlib module) is the oracle here."""
+    import zlib
+
+    return zlib.crc32(_bytes_view(buf), value) & 0xFFFFFFFF
+
+
+def adler32(buf, value: int = 1) -> int:
+    """Adler32.checksum (checksum32.py:125-130) = zlib.adler32."""
+    import zlib
+
+    return zlib.adler32(_bytes_view(buf), value) & 0xFFFFFFFF
+
+
+def crc32c(buf, value: int = 0) -> int:
+    """CRC32C.checksum (checksum32.py:203-209); C restatement in ncoracle.c."""
+    a = np.ascontiguousarray(_bytes_view(buf))
+    return int(_c().nco_crc32c(_ptr(a), a.nbytes, value & 0xFFFFFFFF))
+
+
+def jenkins_lookup3(buf, initval: int = 0) -> int:
+    """jenkins.pyx:93-219; C restatement in ncoracle.c."""
+    a = np.ascontiguousarray(_bytes_view(buf))
+    return int(_c().nco_jenkins_lookup3(_ptr(a), a.nbytes, initval & 0xFFFFFFFF))
+
+
+CHECKSUMS = {"crc32": crc32, "adler32": adler32, "crc32c": crc32c}
+DEFAULT_LOCATION = {"crc32": "start", "adler32": "start", "crc32c": "end"}
+
+
+def checksum32_encode(codec_id: str, buf, location=None) -> np.ndarray:
+    """Checksum32.encode (checksum32.py:56-70): LE32 checksum + payload."""
+    arr = _bytes_view(buf)
+    location = location or DEFAULT_LOCATION[codec_id]
+    cs = np.array([CHECKSUMS[codec_id](arr)], dtype="<u4").view("u1")
+    return np.concatenate([cs, arr] if location == "start" else [arr, cs])
+
+
+def checksum32_decode(codec_id: str, buf, location=None) -> np.ndarray:
+    """Checksum32.decode (checksum32.py:72-88): verify, return the payload."""
+    arr = _bytes_view(buf)
+    location = location or DEFAULT_LOCATION[codec_id]
+    stored, payload = (arr[:4], arr[4:]) if location == "start" else (arr[-4:], arr[:-4])
+    if int(stored.view("<u4")[0]) != CHECKSUMS[codec_id](payload):
+        raise RuntimeError("checksum mismatch")
+    return payload
+
+
+def jenkins_encode(buf, initval=0, prefix=None) -> bytes:
+    """JenkinsLookup3.encode (checksum32.py:160-167)."""
+    arr = _bytes_view(buf)
+    data = arr if prefix is None else np.concatenate([np.frombuffer(prefix, "u1"), arr])
+    return arr.tobytes() + np.array([jenkins_lookup3(data, initval)], "<u4").tobytes()
+
+
+# --------------------------------------------------------------------------
+# AsType (astype.py:46-58), PackBits (packbits.py:33-82)
+# --------------------------------------------------------------------------
+def astype_encode(buf, encode_dtype, decode_dtype) -> np.ndarray:
+    return np.asarray(buf).view(np.dtype(decode_dtype)).astype(np.dtype(encode_dtype))
+
+
+def astype_decode(buf, encode_dtype, decode_dtype) -> np.ndarray:
+    return np.asarray(buf).view(np.dtype(encode_dtype)).astype(np.dtype(decode_dtype))
+
+
+def packbits_encode(buf) -> np.ndarray:
+    arr = np.asarray(buf).view(bool).reshape(-1, order="A")
+    n = arr.size
+    enc = np.empty(n // 8 + (1 if n % 8 else 0) + 1, dtype="u1")
+    enc[0] = (8 - n % 8) if n % 8 else 0
+    enc[1:] = np.packbits(arr)
+    return enc
+
+
+def packbits_decode(buf) -> np.ndarray:
+    enc = np.asarray(buf).view("u1").reshape(-1, order="A")
+    pad = int(enc[0])
+    dec = np.unpackbits(enc[1:])
+    if pad:
+        dec = dec[:-pad]
+    return dec.view(bool)
 
 
 # --------------------------------------------------------------------------

@@ -51,9 +51,20 @@ def load():
         ("shuffle", "Shuffle"),
         ("bitround", "BitRound"),
         ("fletcher32", "Fletcher32"),
+        ("astype", "AsType"),
+        ("packbits", "PackBits"),
     ]:
         mod = importlib.import_module(f"numcodecs.{modname}")
         cls = getattr(mod, clsname)
         setattr(pkg, clsname, cls)
         registry.register_codec(cls)
+    # checksum32.py needs Python >= 3.12 (collections.abc.Buffer, its
+    # pyproject.toml:18 pin) and is not importable on this 3.10; its checksums
+    # are zlib.crc32 / zlib.adler32 and the compiled jenkins.pyx, which the
+    # oracle uses directly, and its framing is pinned by fixture/{crc32,
+    # adler32,crc32c}.
+    try:
+        pkg.jenkins_lookup3 = importlib.import_module("numcodecs.jenkins").jenkins_lookup3
+    except ImportError:
+        pass
     return pkg

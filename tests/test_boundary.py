@@ -32,7 +32,8 @@ HEADER = os.path.join(ROOT, "include", "mcodec.h")
 
 def test_registry_ids():
     assert set(numcodecs_amd.codec_registry) == {
-        "shuffle", "bitround", "delta", "quantize", "fixedscaleoffset", "fletcher32"}
+        "shuffle", "bitround", "delta", "quantize", "fixedscaleoffset", "fletcher32",
+        "crc32", "crc32c", "adler32", "jenkins_lookup3", "astype", "packbits"}
 
 
 def test_registry_errors():
@@ -172,3 +173,29 @@ def test_library_host_queries_need_no_gpu():
     assert lib.mc_fletcher32_workspace(1 << 20) >= 12
     assert lib.mc_delta_decode_workspace(1 << 20, 2, 2) == ((1 << 20) // 4096) * 8
     assert lib.mc_delta_decode_workspace(100, 10, 10) == 0  # float: serial, none
+
+
+# ---- §8f next-row codecs: config surface (no device needed) ----------------
+@pytest.mark.parametrize("stmt", [
+    "CRC32(location='start')", "CRC32(location='end')", "Adler32(location='start')",
+    "Adler32(location='end')", "CRC32C(location='start')", "CRC32C(location='end')",
+    "AsType(encode_dtype='<f4', decode_dtype='<f8')", "AsType(encode_dtype='<i2', decode_dtype='<i4')",
+    "PackBits()", "JenkinsLookup3(initval=0, prefix=None)", "JenkinsLookup3(initval=1230, prefix=None)",
+])
+def test_next_codecs_repr(stmt):
+    check_repr(stmt)
+
+
+def test_next_codecs_config():
+    from numcodecs_amd import CRC32, CRC32C, Adler32, AsType, JenkinsLookup3, PackBits
+
+    for c in (CRC32(), CRC32(location="end"), Adler32(), CRC32C(), CRC32C(location="start"),
+              AsType("<f4", "<f8"), PackBits(), JenkinsLookup3(), JenkinsLookup3(initval=5)):
+        check_config(c)
+    assert CRC32().get_config() == {"id": "crc32"}
+    assert CRC32C().location == "end" and CRC32().location == "start"
+    assert AsType("f4", "f8").get_config() == {"id": "astype", "encode_dtype": "<f4", "decode_dtype": "<f8"}
+    for cls in (CRC32, Adler32, CRC32C):
+        with pytest.raises(ValueError):
+            cls(location="foo")
+    assert JenkinsLookup3(prefix=b"ab").prefix.tolist() == [97, 98]

@@ -1,0 +1,193 @@
+"""GPU parity for the §8f next-row codecs: CRC32 / CRC32C / Adler32 /
+JenkinsLookup3 (checksum32.py), AsType, PackBits -- through the C ABI on the
+device, against the oracle and the reference's fixtures; bit-exact."""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from numcodecs_amd import CRC32, CRC32C, Adler32, AsType, JenkinsLookup3, PackBits, batch, get_codec
+from numcodecs_amd.checksum32 import jenkins_lookup3
+from tests.helpers import check_encode_decode, fixture_cases
+
+pytestmark = pytest.mark.gpu
+RNG = np.random.default_rng(4242)
+
+SIZES = [0, 1, 2, 3, 4, 5, 15, 16, 17, 255, 4095, 4096, 4097, 65535, 65536, 65537,
+         (1 << 20) + 3, (1 << 22) + 16, (1 << 24) + 5]
+REF = {"crc32": oracle.crc32, "crc32c": oracle.crc32c, "adler32": oracle.adler32}
+CODECS = {"crc32": CRC32, "crc32c": CRC32C, "adler32": Adler32}
+
+
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32"])
+def test_checksum_sizes_device(device, codec_id):
+    cls = CODECS[codec_id]
+    for n in SIZES:
+        x = RNG.integers(0, 256, n, dtype=np.uint8)
+        xd = torch.from_numpy(x).to(device)
+        assert cls.checksum(xd) == REF[codec_id](x), (codec_id, n)
+        enc = cls().encode(xd)
+        ref = oracle.checksum32_encode(codec_id, x)
+        assert np.array_equal(enc.cpu().numpy(), ref), (codec_id, n)
+        assert torch.equal(cls().decode(enc), xd)
+
+
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32"])
+def test_checksum_misaligned_and_values(device, codec_id):
+    cls = CODECS[codec_id]
+    base = torch.randint(0, 256, (300000,), dtype=torch.uint8, device=device)
+    for off in (1, 2, 3, 4, 8, 12):
+        for n in (17, 4097, 200001):
+            x = base[off: off + n]
+            assert cls.checksum(x) == REF[codec_id](x.cpu().numpy()), (off, n)
+    x = base[:70001]
+    for v in (0, 1, 7, 0xFFFFFFFF, 0x12345678, 65520 | (65520 << 16)):
+        assert cls.checksum(x, v) == REF[codec_id](x.cpu().numpy(), v), v
+
+
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32"])
+def test_checksum_edge_values(device, codec_id):
+    cls = CODECS[codec_id]
+    for fill in (0, 255):
+        for n in (1, 5552, 5553, 65537, 1 << 20):  # 5552: zlib's NMAX
+            x = torch.full((n,), fill, dtype=torch.uint8, device=device)
+            assert cls.checksum(x) == REF[codec_id](x.cpu().numpy()), (fill, n)
+
+
+def test_checksum_fixtures_device(device):
+    for codec_id, cls in CODECS.items():
+        n = 0
+        for arr, _j, config, enc in fixture_cases(codec_id):
+            c = get_codec(dict(config))
+            assert isinstance(c, cls)
+            got = c.encode(arr)  # host in, host out (staged through the device)
+            assert got.tobytes() == enc, (codec_id, _j)
+            dec = c.decode(enc)
+            assert bytes(dec) == arr.tobytes(order="A")
+            check_encode_decode(arr, c)
+            n += 1
+        assert n == 13
+
+
+@pytest.mark.parametrize("codec", [CRC32(), CRC32(location="end"), Adler32(), Adler32(location="end"),
+                                   CRC32C(), CRC32C(location="start")])
+def test_checksum_errors(device, codec):
+    arr = np.arange(1000, dtype="i4")
+    enc = codec.encode(arr)
+    with pytest.raises(RuntimeError):
+        codec.decode(enc[:-1])
+    with pytest.raises(ValueError):
+        codec.decode(b"000")
+    with pytest.raises(ValueError):
+        codec.encode(np.arange(1000, dtype="i4")[::2])
+    encd = codec.encode(torch.from_numpy(arr).to(device))
+    bad = encd.clone()
+    bad[100] ^= 1
+    with pytest.raises(RuntimeError, match="checksum do not match"):
+        codec.decode(bad)
+
+
+def test_jenkins_kats_device(device):
+    """test_jenkins.py:8-71 through the device kernel."""
+    assert jenkins_lookup3(b"", 0) == 0xDEADBEEF
+    assert jenkins_lookup3(b"", 0xDEADBEEF) == 0xBD5B7DDE
+    assert jenkins_lookup3(b"Four score and seven years ago", 0) == 0x17770551
+    assert jenkins_lookup3(b"Four score and seven years ago", 1) == 0xCD628161
+    assert jenkins_lookup3(b"jenkins", 0) == 202276345
+    s = b"Four score and seven years ago"
+    j = JenkinsLookup3()
+    result = j.encode(s)
+    assert result[-4:] == b"\x51\x05\x77\x17"
+    assert bytes(j.decode(result)) == s
+    j = JenkinsLookup3(initval=1230)
+    result = j.encode(s)
+    assert result[-4:] == b"\xd7Z\xe2\x0e"
+    assert bytes(j.decode(result)) == s
+    j = JenkinsLookup3(initval=0xDEADBEEF, prefix=b"HDF5 prefix")
+    result = j.encode(s)
+    assert result[-4:] == np.array([oracle.jenkins_lookup3(b"HDF5 prefix" + s, 0xDEADBEEF)], "<u4").tobytes()
+    assert bytes(j.decode(result)) == s
+    bad = bytearray(result)
+    bad[3] ^= 0x10
+    with pytest.raises(RuntimeError, match="lookup3 checksum"):
+        j.decode(bytes(bad))
+
+
+def test_jenkins_sizes_device(device):
+    for n in (0, 1, 11, 12, 13, 23, 24, 25, 47, 48, 49, 1000, 65537, (1 << 20) + 7):
+        x = RNG.integers(0, 256, n, dtype=np.uint8)
+        xd = torch.from_numpy(x).to(device)
+        for init in (0, 1230):
+            assert jenkins_lookup3(xd, init) == oracle.jenkins_lookup3(x, init), (n, init)
+        # unaligned device view
+        y = torch.from_numpy(np.concatenate([[7], x]).astype(np.uint8)).to(device)[1:]
+        assert jenkins_lookup3(y) == oracle.jenkins_lookup3(x)
+
+
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32", "jenkins_lookup3"])
+def test_checksum_batches(device, codec_id):
+    ref = {**REF, "jenkins_lookup3": oracle.jenkins_lookup3}[codec_id]
+    for b, n in ((1, 4096), (37, 1000), (64, 65536 + 12), (300, 4096 * 3 + 1), (5, 0)):
+        pad = 16 if n % 2 else 0
+        rows = torch.randint(0, 256, (b, n + pad), dtype=torch.uint8, device=device)[:, :n]
+        sums = batch.checksum32_chunks(rows, codec_id)
+        host = rows.cpu().numpy()
+        assert sums.tolist() == [ref(host[i]) for i in range(b)], (codec_id, b, n)
+        enc = batch.checksum32_encode_chunks(rows, codec_id)
+        codec = get_codec({"id": codec_id})
+        for i in range(b):
+            if codec_id == "jenkins_lookup3":
+                exp = oracle.jenkins_encode(host[i])
+            else:
+                exp = oracle.checksum32_encode(codec_id, host[i]).tobytes()
+            assert enc[i].cpu().numpy().tobytes() == exp, (codec_id, i)
+            assert torch.equal(torch.as_tensor(codec.decode(enc[i])).to(device), rows[i])
+
+
+def test_packbits_fixtures_and_sizes(device):
+    for arr, _j, _config, enc in fixture_cases("packbits"):
+        assert PackBits().encode(arr).tobytes() == enc
+        assert np.array_equal(PackBits().decode(enc), arr.reshape(-1, order="A"))
+        check_encode_decode(arr, PackBits())
+    for n in (0, 1, 7, 8, 9, 63, 64, 65, 127, 128, 129, 1023, 1024, 4097, 1 << 20, (1 << 22) + 5):
+        raw = RNG.integers(0, 4, n, dtype=np.uint8)  # nonzero bytes other than 1 are True
+        x = raw.view(bool)
+        xd = torch.from_numpy(raw).to(device).view(torch.bool)
+        enc = PackBits().encode(xd)
+        assert np.array_equal(enc.cpu().numpy(), oracle.packbits_encode(x)), n
+        dec = PackBits().decode(enc)
+        assert np.array_equal(dec.cpu().numpy(), raw != 0), n
+    # misaligned device input / encoded views
+    base = torch.randint(0, 2, (10000,), dtype=torch.uint8, device=device)
+    for off in (1, 3, 8):
+        x = base[off: off + 9001].view(torch.bool)
+        enc = PackBits().encode(x)
+        assert np.array_equal(enc.cpu().numpy(), oracle.packbits_encode(x.cpu().numpy()))
+        shifted = torch.empty(enc.numel() + off, dtype=torch.uint8, device=device)[off:]
+        shifted.copy_(enc)
+        assert torch.equal(PackBits().decode(shifted), x)
+
+
+def test_astype_fixtures_and_casts(device):
+    for prefix in ("f", "i"):
+        for arr, _j, config, enc in fixture_cases("astype", prefix):
+            c = get_codec(dict(config))
+            assert c.encode(arr).tobytes(order="A") == enc  # fixtures hold memory order
+            dec = c.decode(enc)
+            exp = oracle.astype_decode(np.frombuffer(enc, config["encode_dtype"]), config["encode_dtype"],
+                                       config["decode_dtype"])
+            assert np.array_equal(dec, exp)
+    pairs = [("<f4", "<f8"), ("<i2", "<i4"), ("<u1", "<f8"), ("<i4", "<f4"), ("<f2", "<f4"), ("<f8", "<i8"),
+             ("|b1", "<i4"), ("<i8", "<u2")]
+    for enc_dt, dec_dt in pairs:
+        x = (RNG.standard_normal(100003) * 1e5).astype(dec_dt)
+        xd = torch.from_numpy(x).to(device)
+        got = AsType(enc_dt, dec_dt).encode(xd)
+        with np.errstate(all="ignore"):
+            ref = oracle.astype_encode(x, enc_dt, dec_dt)
+        assert np.array_equal(got.cpu().numpy().view(np.uint8), ref.view(np.uint8)), (enc_dt, dec_dt)
+        back = AsType(enc_dt, dec_dt).decode(got)
+        with np.errstate(all="ignore"):
+            ref_back = oracle.astype_decode(ref, enc_dt, dec_dt)
+        assert np.array_equal(back.cpu().numpy().view(np.uint8), ref_back.view(np.uint8)), (enc_dt, dec_dt)
