@@ -54,6 +54,64 @@ __global__ __launch_bounds__(MC_BLOCK) void k_packbits(const uint8_t *__restrict
   }
 }
 
+// Aligned fast path: a workgroup packs 32 KiB of bools (8 steps of coalesced
+// 16-B loads, 2 packed bytes per lane per step) into 4 KiB staged in LDS one
+// byte later than their packed index, so that the header-shifted output
+// (encoded byte 1 + j = packed byte j) leaves as aligned 16-B stores: lane t
+// stores encoded bytes [P + 16t, P + 16t + 16) = packed [P + 16t - 1, ...).
+// The byte before the block (packed P - 1, or the header for block 0) is
+// recomputed by thread 0 from the 8 bools before the block.
+constexpr int PB_STEPS = 8;
+constexpr size_t PB_SRC = (size_t)PB_STEPS * MC_BLOCK * 16;  // 32 KiB of bools
+constexpr size_t PB_OUT = PB_SRC / 8;                          // 4 KiB packed
+
+__global__ __launch_bounds__(MC_BLOCK) void k_packbits_blk(const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst, size_t n,
+                                                           size_t out_bytes) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[PB_OUT + 8];
+  const size_t B = (size_t)blockIdx.x * PB_SRC, P = (size_t)blockIdx.x * PB_OUT;
+  const int t = threadIdx.x;
+  mc_u32x4 v[PB_STEPS];
+#pragma unroll
+  for (int k = 0; k < PB_STEPS; ++k) {
+    const size_t pos = B + (size_t)k * MC_BLOCK * 16 + 16 * (size_t)t;
+    if (pos + 16 <= n) {
+      v[k] = mc_ld16<true>(src + pos);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 16; ++j)
+        if (pos + j < n) w[j >> 2] |= (uint32_t)src[pos + j] << (8 * (j & 3));
+      v[k] = mc_u32x4{w[0], w[1], w[2], w[3]};
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PB_STEPS; ++k) {
+    const uint32_t lo = pack8(((uint64_t)v[k].y << 32) | v[k].x);
+    const uint32_t hi = pack8(((uint64_t)v[k].w << 32) | v[k].z);
+    *reinterpret_cast<uint16_t *>(lds + 4 + 2 * (k * MC_BLOCK + t)) = (uint16_t)(lo | (hi << 8));
+  }
+  if (t == 0)
+    lds[3] = blockIdx.x == 0 ? (uint8_t)((8 - n % 8) % 8)
+                             : (uint8_t)pack8(*reinterpret_cast<const uint64_t *>(src + B - 8));
+  __syncthreads();
+  const uint32_t *l32 = reinterpret_cast<const uint32_t *>(lds);
+  uint32_t d[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) d[k] = l32[4 * t + k];
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], 3);
+  const size_t o = P + 16 * (size_t)t;
+  if (o + 16 <= out_bytes) {
+    mc_st16<true>(dst + o, mc_u32x4{w[0], w[1], w[2], w[3]});
+  } else {
+    for (int q = 0; q < 16 && o + q < out_bytes; ++q) dst[o + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+  }
+  // the block's last packed byte belongs to encoded byte P + 4096, which the
+  // next block writes; the last block writes it itself
+  if (t == 0 && blockIdx.x + 1 == gridDim.x && P + PB_OUT < out_bytes) dst[P + PB_OUT] = lds[PB_OUT + 3];
+}
+
 // lane g writes bools [64g, 64g + 64) from packed bytes 8g..8g+7, which sit at
 // encoded offsets 1 + 8g .. 8 + 8g (src = the encoded buffer, header first).
 __global__ __launch_bounds__(MC_BLOCK) void k_unpackbits(const uint8_t *__restrict__ src,
@@ -95,6 +153,13 @@ extern "C" {
 int mc_packbits(const void *src, void *dst, size_t n, mc_stream_t stream) {
   if (!dst || (n && !src)) return MC_EINVAL;
   const size_t out_bytes = 1 + (n + 7) / 8;
+  if (n > 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    const size_t blocks = (n + PB_SRC - 1) / PB_SRC;
+    if (blocks > 0x7fffffffu) return MC_EINVAL;
+    k_packbits_blk<<<(unsigned)blocks, MC_BLOCK, 0, (hipStream_t)stream>>>(
+        static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), n, out_bytes);
+    return mc_last_launch();
+  }
   const size_t lanes = (out_bytes + 15) / 16;
   const size_t grid = (lanes + MC_BLOCK - 1) / MC_BLOCK;
   if (grid > 0x7fffffffu) return MC_EINVAL;

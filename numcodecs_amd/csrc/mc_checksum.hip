@@ -30,6 +30,8 @@
 // single-thread speed (documented in DESIGN.md).
 #include "mc_common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -409,20 +411,48 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
   if (L > 0) {
     const size_t nb = (L - 1) / 12;  // full mixing blocks ("while length > 12")
     size_t blk = 0;
-    if (plen == 0 && ((uintptr_t)s & 3) == 0) {
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(s);
-      for (; blk + 4 <= nb; blk += 4) {
-        uint32_t q[12];
+    if (plen == 0 && ((uintptr_t)s & 15) == 0) {
+      // 16 blocks (192 B = 12 x 16-B loads) per group, the next group's loads
+      // in flight while the current one mixes
+      constexpr size_t G = 16;
+      const mc_u32x4 *v4 = reinterpret_cast<const mc_u32x4 *>(s);
+      const size_t ng = nb / G;
+      mc_u32x4 cur[12];
+      if (ng) {
 #pragma unroll
-        for (int j = 0; j < 12; ++j) q[j] = w[3 * blk + j];
+        for (int j = 0; j < 12; ++j) cur[j] = v4[j];
+      }
+      for (size_t gi = 0; gi < ng; ++gi) {
+        mc_u32x4 nxt[12];
+        if (gi + 1 < ng) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+          for (int j = 0; j < 12; ++j) nxt[j] = v4[12 * (gi + 1) + j];
+        }
+        uint32_t q[48];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+          q[4 * j] = cur[j].x; q[4 * j + 1] = cur[j].y; q[4 * j + 2] = cur[j].z; q[4 * j + 3] = cur[j].w;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
           a += q[3 * r];
           b += q[3 * r + 1];
           c += q[3 * r + 2];
           jmix(a, b, c);
         }
+#pragma unroll
+        for (int j = 0; j < 12; ++j) cur[j] = nxt[j];
       }
+      blk = ng * G;
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s);
+      for (; blk < nb; ++blk) {
+        a += w[3 * blk];
+        b += w[3 * blk + 1];
+        c += w[3 * blk + 2];
+        jmix(a, b, c);
+      }
+    } else if (plen == 0 && ((uintptr_t)s & 3) == 0) {
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s);
       for (; blk < nb; ++blk) {
         a += w[3 * blk];
         b += w[3 * blk + 1];
@@ -455,10 +485,29 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-constexpr unsigned CK_MAX_GRID = 2048;
+// Tuning knobs (read once): MCODEC_CK_K = tile size in STEP units for chunks
+// of >= 64 KiB (4, 8 or 16), MCODEC_CK_GRID = persistent grid cap.
+inline int ck_env(const char *name, int def) {
+  const char *v = getenv(name);
+  return v ? atoi(v) : def;
+}
+inline int ck_kbig() {
+  static const int k = [] {
+    const int e = ck_env("MCODEC_CK_K", 16);
+    return (e == 4 || e == 8 || e == 16) ? e : 16;
+  }();
+  return k;
+}
+inline unsigned ck_grid_cap() {
+  static const unsigned g = [] {
+    const int e = ck_env("MCODEC_CK_GRID", 2048);
+    return e > 0 ? (unsigned)e : 2048u;
+  }();
+  return g;
+}
 
-// tile size (in STEP units) for a chunk: K = 1 below 64 KiB, else 16
-inline int ck_k(size_t n) { return n < (size_t)16 * STEP ? 1 : 16; }
+// tile size (in STEP units) for a chunk: K = 1 below 64 KiB
+inline int ck_k(size_t n) { return n < (size_t)16 * STEP ? 1 : ck_kbig(); }
 inline size_t ck_tiles(size_t n, int K) {
   const size_t tb = (size_t)K * STEP;
   return n ? (n + tb - 1) / tb : 1;
@@ -471,7 +520,7 @@ inline int align_class(const void *p, size_t stride, size_t nchunks) {
 template <int KIND, int K, bool COPY, int ALS, int ALD>
 void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
                   size_t total, uint32_t *parts, hipStream_t st) {
-  const unsigned grid = (unsigned)(total < CK_MAX_GRID ? total : CK_MAX_GRID);
+  const unsigned grid = (unsigned)(total < ck_grid_cap() ? total : ck_grid_cap());
   k_ck_tiles<KIND, K, COPY, ALS, ALD><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts);
 }
 
@@ -502,12 +551,20 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;
   uint32_t *parts = static_cast<uint32_t *>(ws);
-  if (K == 1) {
-    dispatch_tiles<KIND, 1>(s, ss, d, ds, nchunks, n, tpc, parts, st);
-    k_ck_finalize<KIND, 1><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out, footer, fs);
-  } else {
-    dispatch_tiles<KIND, 16>(s, ss, d, ds, nchunks, n, tpc, parts, st);
-    k_ck_finalize<KIND, 16><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out, footer, fs);
+  switch (K) {
+#define MC_CK_CASE(KK)                                                                         \
+  case KK:                                                                                     \
+    dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, st);                        \
+    k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out,  \
+                                                                    footer, fs);               \
+    break;
+    MC_CK_CASE(1)
+    MC_CK_CASE(4)
+    MC_CK_CASE(8)
+    MC_CK_CASE(16)
+#undef MC_CK_CASE
+    default:
+      return MC_EINVAL;
   }
   return mc_last_launch();
 }
