@@ -292,6 +292,16 @@ def next_row_workloads(dev):
     out["packbits_256MiB_encode_GBps"] = round((CHUNK + CHUNK // 8) / t / 1e9, 1)
     t = timed(lambda: PackBits().decode(enc))
     out["packbits_256MiB_decode_GBps"] = round((CHUNK + CHUNK // 8) / t / 1e9, 1)
+    from numcodecs_amd import blosc_shuffle as bsh
+
+    x4 = torch.randn(CHUNK // 4, device=dev)
+    for mode, name in ((bsh.SHUFFLE, "shuffle"), (bsh.BITSHUFFLE, "bitshuffle")):
+        enc4 = bsh.shuffle(x4, 4, 256 * 1024, mode)
+        t_e = timed(lambda: bsh.shuffle(x4, 4, 256 * 1024, mode))
+        t_d = timed(lambda: bsh.unshuffle(enc4, 4, 256 * 1024, mode))
+        out[f"blosc_{name}_f4_256KiB_blocks_enc_GBps"] = round(2 * CHUNK / t_e / 1e9, 1)
+        out[f"blosc_{name}_f4_256KiB_blocks_dec_GBps"] = round(2 * CHUNK / t_d / 1e9, 1)
+    del x4, enc4
     x64 = torch.randn(CHUNK // 8, device=dev, dtype=torch.float64)
     t = timed(lambda: AsType("<f4", "<f8").encode(x64))
     out["astype_f8_to_f4_256MiB_GBps"] = round(1.5 * CHUNK / t / 1e9, 1)

@@ -32,6 +32,8 @@
  *                                    zlib.adler32), CRC32C (:189-209), JenkinsLookup3
  *                                    (:133-181 over jenkins.pyx:93-325)
  *   mc_packbits / mc_unpackbits .... packbits.py:33-82 PackBits.encode/decode
+ *   mc_blosc_filter ................ blosc.pyx:67-71,211-326 SHUFFLE / BITSHUFFLE as
+ *                                    c-blosc applies them per block (shuffle.c)
  *   *_batch ........................ no reference counterpart: the Zarr caller loops
  *                                    Codec.encode per chunk; these run B equal-size
  *                                    chunks in one launch (chunk b at base + b*stride).
@@ -248,6 +250,19 @@ int mc_packbits(const void *src, void *dst, size_t n, mc_stream_t stream);
  * 8 * (src_bytes - 1) - src[0] (read by the caller). */
 int mc_unpackbits(const void *src, size_t src_bytes, void *dst, size_t n,
                   mc_stream_t stream);
+
+/* ---- Blosc shuffle filters (blosc.pyx:67-71, c-blosc shuffle.c) ---------- */
+/* Filter a buffer block by block exactly as Blosc does before/after its
+ * compressor: the buffer is cut into blocksize-byte blocks (last one
+ * shorter); mode MC_BLOSC_SHUFFLE byte-transposes each block's
+ * (bsize/typesize, typesize) matrix and copies the bsize % typesize trailing
+ * bytes; MC_BLOSC_BITSHUFFLE bit-transposes blocks whose element count is a
+ * multiple of 8 (bit k of byte j of element i -> bit i%8 of byte i/8 of
+ * plane 8j+k) and copies the others; MC_BLOSC_NOSHUFFLE copies.
+ * forward = 1 filters (compress side), 0 inverts (decompress side). */
+enum mc_blosc_mode { MC_BLOSC_NOSHUFFLE = 0, MC_BLOSC_SHUFFLE = 1, MC_BLOSC_BITSHUFFLE = 2 };
+int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize,
+                    size_t blocksize, int mode, int forward, mc_stream_t stream);
 
 /* ---- tuning / measurement hooks (bench.py) ----------------------------- */
 /* Shuffle with an explicit kernel variant and grid (0 = default); used by

@@ -56,7 +56,8 @@ from .packbits import PackBits
 
 register_codec(PackBits)
 
-from . import batch  # noqa: E402,F401  (batched chunk API and fused pipelines)
+from . import batch  # noqa: E402,F401
+from . import blosc_shuffle  # noqa: E402,F401  (Blosc's per-block shuffle filters)  (batched chunk API and fused pipelines)
 
 __version__ = "0.1.0"
 
@@ -76,6 +77,7 @@ __all__ = [
     "Shuffle",
     "UnknownCodecError",
     "batch",
+    "blosc_shuffle",
     "codec_registry",
     "get_codec",
     "register_codec",

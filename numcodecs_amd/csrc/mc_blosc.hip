@@ -1,0 +1,178 @@
+// mc_blosc.hip -- Blosc's shuffle filters applied block by block (SURVEY.md
+// §8f row 2; blosc.pyx:67-71 NOSHUFFLE/SHUFFLE/BITSHUFFLE, :211-326), with
+// c-blosc 1.x semantics pinned by the reference's fixture/blosc frames
+// (oracle/blosc.py):
+//   * the buffer is cut into `blocksize`-byte blocks (the last one shorter),
+//     each filtered on its own, E = bsize / typesize elements per block;
+//   * SHUFFLE: byte transpose of the (E, typesize) matrix, the bsize %
+//     typesize trailing bytes copied -- run on the Shuffle kernels
+//     (mc_shuffle.hip) as a batch of equal blocks plus the last block;
+//   * BITSHUFFLE (bitshuffle's bshuf_trans_bit_elem): if E % 8 == 0, bit k of
+//     byte j of element i -> bit i%8 of byte i/8 of bit-plane 8j+k (planes of
+//     E/8 bytes); otherwise the block is copied unchanged.
+//
+// Bit-shuffle kernel: a workgroup owns G groups of 8 elements of one block
+// (G*8*typesize <= 32 KiB).  The elements are staged in LDS with coalesced
+// loads; thread t gathers, for every byte position j, byte j of its 8
+// elements into a u64 and transposes that 8x8 bit matrix with three
+// delta-swaps, giving the 8 plane bytes (8j+k, t); these are staged in LDS
+// plane-major and leave as coalesced per-plane runs of G bytes.  The inverse
+// runs the same steps backwards (the 8x8 transpose is an involution).
+#include "mc_common.h"
+
+namespace {
+
+MC_DEV uint64_t tr8x8(uint64_t x) {  // byte r bit c  <->  byte c bit r
+  uint64_t t;
+  t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+  x = x ^ t ^ (t << 7);
+  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+  x = x ^ t ^ (t << 14);
+  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+  x = x ^ t ^ (t << 28);
+  return x;
+}
+
+constexpr int BS_LDS = 32768;  // bytes of element data per workgroup
+
+inline unsigned groups_per_wg(size_t ts) {
+  const size_t g = BS_LDS / (8 * ts);
+  return (unsigned)(g < MC_BLOCK ? g : MC_BLOCK);
+}
+
+// copy [lo, hi) of a block, spread over the workgroup
+MC_DEV void wg_copy(const uint8_t *s, uint8_t *d, size_t lo, size_t hi) {
+  for (size_t i = lo + threadIdx.x; i < hi; i += MC_BLOCK) d[i] = s[i];
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle(const uint8_t *__restrict__ src,
+                                                         uint8_t *__restrict__ dst, size_t nbytes,
+                                                         unsigned ts, size_t blocksize,
+                                                         unsigned G) {
+  __shared__ __attribute__((aligned(16))) uint8_t elem[BS_LDS];
+  __shared__ __attribute__((aligned(16))) uint8_t plane[BS_LDS];
+  const size_t b0 = (size_t)blockIdx.x * blocksize;
+  const size_t bsize = nbytes - b0 < blocksize ? nbytes - b0 : blocksize;
+  const uint8_t *s = src + b0;
+  uint8_t *d = dst + b0;
+  const size_t E = bsize / ts;
+  const size_t wg_bytes = (size_t)G * 8 * ts;
+  const size_t lo = (size_t)blockIdx.y * wg_bytes;
+  if (E % 8) {  // c-blosc copies such blocks unchanged
+    if (lo < bsize) wg_copy(s, d, lo, lo + wg_bytes < bsize ? lo + wg_bytes : bsize);
+    return;
+  }
+  if (blockIdx.y == 0) wg_copy(s, d, E * ts, bsize);  // trailing bytes, if any
+  const size_t ng = E / 8, g0 = (size_t)blockIdx.y * G;
+  if (g0 >= ng) return;
+  const unsigned Gt = (unsigned)(ng - g0 < G ? ng - g0 : G);
+  const unsigned n8 = 8 * ts;  // planes
+  const size_t pstride = E / 8;
+  const int t = threadIdx.x;
+  if (FWD) {
+    const size_t off = g0 * n8, len = (size_t)Gt * n8;
+    if ((((uintptr_t)(s + off)) & 15) == 0 && (len & 15) == 0) {
+      for (size_t i = 16 * (size_t)t; i < len; i += 16 * MC_BLOCK)
+        *reinterpret_cast<mc_u32x4 *>(elem + i) = mc_ld16<true>(s + off + i);
+    } else {
+      for (size_t i = t; i < len; i += MC_BLOCK) elem[i] = s[off + i];
+    }
+    __syncthreads();
+    if (t < (int)Gt) {
+      for (unsigned j = 0; j < ts; ++j) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x |= (uint64_t)elem[(8 * t + r) * ts + j] << (8 * r);
+        x = tr8x8(x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) plane[(8 * j + k) * Gt + t] = (uint8_t)(x >> (8 * k));
+      }
+    }
+    __syncthreads();
+    for (unsigned i = t; i < n8 * Gt; i += MC_BLOCK) {
+      const unsigned p = i / Gt, q = i - p * Gt;
+      d[p * pstride + g0 + q] = plane[i];
+    }
+  } else {
+    for (unsigned i = t; i < n8 * Gt; i += MC_BLOCK) {
+      const unsigned p = i / Gt, q = i - p * Gt;
+      plane[i] = s[p * pstride + g0 + q];
+    }
+    __syncthreads();
+    if (t < (int)Gt) {
+      for (unsigned j = 0; j < ts; ++j) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x |= (uint64_t)plane[(8 * j + k) * Gt + t] << (8 * k);
+        x = tr8x8(x);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) elem[(8 * t + r) * ts + j] = (uint8_t)(x >> (8 * r));
+      }
+    }
+    __syncthreads();
+    const size_t off = g0 * n8, len = (size_t)Gt * n8;
+    if ((((uintptr_t)(d + off)) & 15) == 0 && (len & 15) == 0) {
+      for (size_t i = 16 * (size_t)t; i < len; i += 16 * MC_BLOCK)
+        mc_st16<true>(d + off + i, *reinterpret_cast<const mc_u32x4 *>(elem + i));
+    } else {
+      for (size_t i = t; i < len; i += MC_BLOCK) d[off + i] = elem[i];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, size_t blocksize,
+                    int mode, int forward, mc_stream_t stream) {
+  if (nbytes == 0) return MC_OK;
+  if (!src || !dst || typesize < 1 || typesize > 255 || blocksize < 1) return MC_EINVAL;
+  if (mode != MC_BLOSC_NOSHUFFLE && mode != MC_BLOSC_SHUFFLE && mode != MC_BLOSC_BITSHUFFLE)
+    return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const size_t nblocks = (nbytes + blocksize - 1) / blocksize;
+  if (mode == MC_BLOSC_NOSHUFFLE || (mode == MC_BLOSC_SHUFFLE && typesize == 1))
+    return mc_hip_status(hipMemcpyAsync(d, s, nbytes, hipMemcpyDeviceToDevice, st));
+  if (mode == MC_BLOSC_SHUFFLE) {
+    // full blocks as one batch on the Shuffle kernels, then the last block
+    const size_t full = nbytes / blocksize, body = blocksize / typesize * typesize;
+    int rc = MC_OK;
+    if (full) {
+      rc = forward ? mc_shuffle_batch(s, blocksize, d, blocksize, full, body, typesize, stream)
+                   : mc_unshuffle_batch(s, blocksize, d, blocksize, full, body, typesize, stream);
+      if (rc != MC_OK) return rc;
+      if (body < blocksize)  // trailing bytes of every full block
+        rc = mc_hip_status(hipMemcpy2DAsync(d + body, blocksize, s + body, blocksize,
+                                            blocksize - body, full, hipMemcpyDeviceToDevice, st));
+      if (rc != MC_OK) return rc;
+    }
+    const size_t last = nbytes - full * blocksize;
+    if (last) {
+      const size_t lb = last / typesize * typesize;
+      const uint8_t *ls = s + full * blocksize;
+      uint8_t *ld = d + full * blocksize;
+      if (lb) {
+        rc = forward ? mc_shuffle(ls, ld, lb, typesize, stream) : mc_unshuffle(ls, ld, lb, typesize, stream);
+        if (rc != MC_OK) return rc;
+      }
+      if (lb < last)
+        rc = mc_hip_status(hipMemcpyAsync(ld + lb, ls + lb, last - lb, hipMemcpyDeviceToDevice, st));
+    }
+    return rc;
+  }
+  const unsigned G = groups_per_wg(typesize);
+  const size_t per_wg = (size_t)G * 8 * typesize;
+  const size_t span = blocksize < nbytes ? blocksize : nbytes;
+  const size_t tiles = (span + per_wg - 1) / per_wg;  // workgroups per block
+  if (tiles > 65535 || nblocks > 0x7fffffffu) return MC_EINVAL;
+  const dim3 grid((unsigned)nblocks, (unsigned)tiles);
+  if (forward) k_bitshuffle<true><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
+  else k_bitshuffle<false><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
+  return mc_last_launch();
+}
+
+}  // extern "C"

@@ -191,3 +191,45 @@ def test_astype_fixtures_and_casts(device):
         with np.errstate(all="ignore"):
             ref_back = oracle.astype_decode(ref, enc_dt, dec_dt)
         assert np.array_equal(back.cpu().numpy().view(np.uint8), ref_back.view(np.uint8)), (enc_dt, dec_dt)
+
+
+# ---------------------------------------------------------------------------
+# Blosc shuffle filters (numcodecs_amd.blosc_shuffle) vs fixture/blosc frames
+# ---------------------------------------------------------------------------
+def test_blosc_filters_fixture_frames(device):
+    from numcodecs_amd import blosc_shuffle as bsh
+    from oracle import blosc
+
+    n = 0
+    for arr, _j, _config, frame in fixture_cases("blosc"):
+        try:
+            flags, ts, bs, blocks = blosc.frame_filtered_blocks(frame)
+        except NotImplementedError:
+            continue
+        if blocks is None:
+            continue
+        mode = 2 if flags & blosc.BLOSC_DOBITSHUFFLE else 1 if flags & blosc.BLOSC_DOSHUFFLE else 0
+        raw = arr.tobytes(order="A")
+        filtered = b"".join(blocks)
+        got = bsh.shuffle(np.frombuffer(raw, "u1"), ts, bs, mode)
+        assert got.tobytes() == filtered, (_j, ts, bs, mode)
+        back = bsh.unshuffle(np.frombuffer(filtered, "u1"), ts, bs, mode)
+        assert back.tobytes() == raw
+        n += 1
+    assert n == 84
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_blosc_filters_sizes(device, mode):
+    from numcodecs_amd import blosc_shuffle as bsh
+    from oracle import blosc
+
+    for ts in (1, 2, 3, 4, 8, 16, 24):
+        for nel, bs in ((0, 256), (1, 256), (8, 64 * ts), (1000, 8 * ts * 16), (4096 + 5, 65536),
+                        (100003, 32768), (262144, 1 << 20)):
+            raw = RNG.integers(0, 256, nel * ts + (nel % 5 if ts > 1 else 0), dtype=np.uint8)
+            xd = torch.from_numpy(raw).to(device)
+            got = bsh.shuffle(xd, ts, bs, mode)
+            ref = blosc.blosc_filter(raw, ts, bs, mode)
+            assert got.cpu().numpy().tobytes() == ref, (ts, nel, bs, mode)
+            assert torch.equal(bsh.unshuffle(got, ts, bs, mode), xd), (ts, nel, bs, mode)

@@ -132,3 +132,52 @@ def test_oracle_matches_reference_jenkins_astype_packbits():
     for enc_dt, dec_dt in (("<f4", "<f8"), ("<i2", "<i4"), ("<u1", "<f8"), ("<i4", "<f4")):
         x = (RNG.standard_normal(257) * 1e5).astype(dec_dt)
         assert np.array_equal(nc.AsType(enc_dt, dec_dt).encode(x), oracle.astype_encode(x, enc_dt, dec_dt))
+
+
+# ---------------------------------------------------------------------------
+# Blosc shuffle framing (oracle/blosc.py) pinned by fixture/blosc frames
+# ---------------------------------------------------------------------------
+def _blosc_cases():
+    from oracle import blosc
+
+    for arr, j, config, frame in fixture_cases("blosc"):
+        flags, ts, bs, blocks = (None, None, None, None)
+        try:
+            flags, ts, bs, blocks = blosc.frame_filtered_blocks(frame)
+        except NotImplementedError:
+            continue
+        yield arr, j, config, flags, ts, bs, blocks
+
+
+def test_fixture_blosc_filters_bytes_exact():
+    from oracle import blosc
+
+    counts = {1: 0, 2: 0, 0: 0}
+    for arr, _j, config, flags, ts, bs, blocks in _blosc_cases():
+        raw = arr.tobytes(order="A")
+        if blocks is None:  # memcpyed frame: stored raw
+            continue
+        mode = 2 if flags & blosc.BLOSC_DOBITSHUFFLE else 1 if flags & blosc.BLOSC_DOSHUFFLE else 0
+        if config["shuffle"] in (1, 2):
+            assert mode == config["shuffle"] or (ts == 1 and mode == 0)
+        filtered = b"".join(blocks)
+        if mode == 0:
+            assert filtered == raw
+        else:
+            assert blosc.blosc_filter(raw, ts, bs, mode) == filtered, (_j, ts, bs, mode)
+            assert blosc.blosc_filter(filtered, ts, bs, mode, forward=False) == raw
+        counts[mode] += 1
+    assert counts == {0: 16, 1: 55, 2: 13}, counts  # 84 LZ4 frames walked
+
+
+def test_blosc_filter_roundtrip_edges():
+    from oracle import blosc
+
+    for ts in (1, 2, 3, 4, 8, 16):
+        for n in (0, 1, 7, 64, 1000, 4099):
+            raw = RNG.integers(0, 256, n * ts + (n % 3), dtype=np.uint8).tobytes()
+            for bs in (8 * ts, 255, 4096):
+                for mode in (1, 2):
+                    enc = blosc.blosc_filter(raw, ts, bs, mode)
+                    assert len(enc) == len(raw)
+                    assert blosc.blosc_filter(enc, ts, bs, mode, forward=False) == raw
