@@ -121,6 +121,137 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle(const uint8_t *__restri
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Fast path for typesize ES in {1, 2, 4, 8} and blocks whose element count is
+// a multiple of 32 (every plane then starts dword aligned): thread t owns 4
+// consecutive groups of 8 elements (32*ES contiguous bytes) and writes one
+// dword (4 groups) of each of its 8*ES planes -- 256 contiguous bytes per
+// plane per wave store.  The element side moves through LDS with coalesced
+// 16-B global accesses; the LDS image is XOR-swizzled per owner thread
+// (slot i of thread t at 2ES*t + (i ^ (t & (2ES-1)))) so that the owner's
+// ds_read/write_b128 sweep is at most 2-way bank conflicted.  Byte j of
+// element e sits at bit 8*((e*ES + j) % 4) of dword (e*ES + j)/4 -- all
+// compile-time, so the gathers become v_bfe/v_perm.
+// ---------------------------------------------------------------------------
+constexpr int BF_GPT = 4;                     // groups per thread
+constexpr int BF_GROUPS = BF_GPT * MC_BLOCK;  // groups per workgroup
+
+template <int ES>
+MC_DEV int bf_slot(int t, int i) {
+  return 2 * ES * t + (i ^ (t & (2 * ES - 1)));
+}
+
+template <int ES>
+MC_DEV uint32_t bf_byte(const uint32_t (&w)[8 * ES], int e, int j) {
+  const int b = e * ES + j;
+  return (w[b >> 2] >> (8 * (b & 3))) & 0xffu;
+}
+
+template <int ES, bool FWD>
+__global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__restrict__ src,
+                                                              uint8_t *__restrict__ dst,
+                                                              size_t blocksize) {
+  constexpr int SLOTS = 2 * ES;  // 16-B slots per thread
+  __shared__ __attribute__((aligned(16))) mc_u32x4 lds[SLOTS * MC_BLOCK];
+  const size_t E = blocksize / ES, ng = E / 8, pstride = E / 8;
+  const size_t gw = (size_t)blockIdx.y * BF_GROUPS;  // first group of the workgroup
+  if (gw >= ng) return;
+  const size_t gcount = ng - gw < (size_t)BF_GROUPS ? ng - gw : BF_GROUPS;  // multiple of 4
+  const int nthr = (int)(gcount / BF_GPT);
+  const int nslots = nthr * SLOTS;
+  const int t = threadIdx.x;
+  const uint8_t *s = src + (size_t)blockIdx.x * blocksize;
+  uint8_t *d = dst + (size_t)blockIdx.x * blocksize;
+  const size_t ebase = gw * 8 * ES;  // byte offset of the workgroup's elements
+  if (FWD) {
+    for (int q = t; q < nslots; q += MC_BLOCK)
+      lds[bf_slot<ES>(q / SLOTS, q % SLOTS)] = mc_ld16<true>(s + ebase + 16 * (size_t)q);
+    __syncthreads();
+    if (t >= nthr) return;
+    uint32_t w[8 * ES];
+#pragma unroll
+    for (int i = 0; i < SLOTS; ++i) {
+      const mc_u32x4 v = lds[bf_slot<ES>(t, i)];
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+    uint8_t *pd = d + gw + BF_GPT * (size_t)t;
+#pragma unroll
+    for (int j = 0; j < ES; ++j) {
+      uint64_t T[BF_GPT];
+#pragma unroll
+      for (int g = 0; g < BF_GPT; ++g) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x |= (uint64_t)bf_byte<ES>(w, 8 * g + r, j) << (8 * r);
+        T[g] = tr8x8(x);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int g = 0; g < BF_GPT; ++g) o |= (uint32_t)((T[g] >> (8 * k)) & 0xffu) << (8 * g);
+        __builtin_nontemporal_store(o, reinterpret_cast<uint32_t *>(pd + (size_t)(8 * j + k) * pstride));
+      }
+    }
+  } else {
+    uint32_t w[8 * ES];
+    if (t < nthr) {
+      const uint8_t *ps = s + gw + BF_GPT * (size_t)t;
+      uint32_t pl[8 * ES];
+#pragma unroll
+      for (int p = 0; p < 8 * ES; ++p)
+        pl[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)p * pstride));
+#pragma unroll
+      for (int i = 0; i < 8 * ES; ++i) w[i] = 0;
+#pragma unroll
+      for (int j = 0; j < ES; ++j) {
+#pragma unroll
+        for (int g = 0; g < BF_GPT; ++g) {
+          uint64_t x = 0;  // byte k = plane 8j+k's byte for group g
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x |= (uint64_t)((pl[8 * j + k] >> (8 * g)) & 0xffu) << (8 * k);
+          x = tr8x8(x);  // byte r = byte j of element 8g+r
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int b = (8 * g + r) * ES + j;
+            w[b >> 2] |= (uint32_t)((x >> (8 * r)) & 0xffu) << (8 * (b & 3));
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SLOTS; ++i)
+        lds[bf_slot<ES>(t, i)] = mc_u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+    }
+    __syncthreads();
+    for (int q = t; q < nslots; q += MC_BLOCK)
+      mc_st16<true>(d + ebase + 16 * (size_t)q, lds[bf_slot<ES>(q / SLOTS, q % SLOTS)]);
+  }
+}
+
+template <int ES>
+void launch_bitshuffle_fast(const uint8_t *s, uint8_t *d, size_t nfull, size_t blocksize, bool fwd,
+                            hipStream_t st) {
+  const size_t ng = blocksize / ES / 8;
+  const dim3 grid((unsigned)nfull, (unsigned)((ng + BF_GROUPS - 1) / BF_GROUPS));
+  if (fwd) k_bitshuffle_fast<ES, true><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);
+  else k_bitshuffle_fast<ES, false><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);
+}
+
+inline int launch_bitshuffle_generic(const uint8_t *s, uint8_t *d, size_t nbytes, size_t typesize,
+                                     size_t blocksize, bool fwd, hipStream_t st) {
+  const size_t nblocks = (nbytes + blocksize - 1) / blocksize;
+  const unsigned G = groups_per_wg(typesize);
+  const size_t per_wg = (size_t)G * 8 * typesize;
+  const size_t span = blocksize < nbytes ? blocksize : nbytes;
+  const size_t tiles = (span + per_wg - 1) / per_wg;  // workgroups per block
+  if (tiles > 65535 || nblocks > 0x7fffffffu) return MC_EINVAL;
+  const dim3 grid((unsigned)nblocks, (unsigned)tiles);
+  if (fwd) k_bitshuffle<true><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
+  else k_bitshuffle<false><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
+  return mc_last_launch();
+}
+
 }  // namespace
 
 extern "C" {
@@ -134,7 +265,6 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
   hipStream_t st = (hipStream_t)stream;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
-  const size_t nblocks = (nbytes + blocksize - 1) / blocksize;
   if (mode == MC_BLOSC_NOSHUFFLE || (mode == MC_BLOSC_SHUFFLE && typesize == 1))
     return mc_hip_status(hipMemcpyAsync(d, s, nbytes, hipMemcpyDeviceToDevice, st));
   if (mode == MC_BLOSC_SHUFFLE) {
@@ -164,15 +294,25 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
     }
     return rc;
   }
-  const unsigned G = groups_per_wg(typesize);
-  const size_t per_wg = (size_t)G * 8 * typesize;
-  const size_t span = blocksize < nbytes ? blocksize : nbytes;
-  const size_t tiles = (span + per_wg - 1) / per_wg;  // workgroups per block
-  if (tiles > 65535 || nblocks > 0x7fffffffu) return MC_EINVAL;
-  const dim3 grid((unsigned)nblocks, (unsigned)tiles);
-  if (forward) k_bitshuffle<true><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
-  else k_bitshuffle<false><<<grid, MC_BLOCK, 0, st>>>(s, d, nbytes, (unsigned)typesize, blocksize, G);
-  return mc_last_launch();
+  // bit-shuffle: full blocks on the fast kernel when the layout allows it,
+  // the rest (and every other typesize) on the generic one
+  const bool fwd = forward != 0;
+  const size_t nfull = nbytes / blocksize;
+  const bool fast_ts = typesize == 1 || typesize == 2 || typesize == 4 || typesize == 8;
+  const bool fast = fast_ts && nfull > 0 && blocksize % (32 * typesize) == 0 &&
+                    ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0 &&
+                    blocksize / typesize / 8 / BF_GROUPS < 65536 && nfull <= 0x7fffffffu;
+  if (!fast) return launch_bitshuffle_generic(s, d, nbytes, typesize, blocksize, fwd, st);
+  switch (typesize) {
+    case 1: launch_bitshuffle_fast<1>(s, d, nfull, blocksize, fwd, st); break;
+    case 2: launch_bitshuffle_fast<2>(s, d, nfull, blocksize, fwd, st); break;
+    case 4: launch_bitshuffle_fast<4>(s, d, nfull, blocksize, fwd, st); break;
+    default: launch_bitshuffle_fast<8>(s, d, nfull, blocksize, fwd, st); break;
+  }
+  const int rc = mc_last_launch();
+  if (rc != MC_OK || nbytes == nfull * blocksize) return rc;
+  const size_t off = nfull * blocksize;
+  return launch_bitshuffle_generic(s + off, d + off, nbytes - off, typesize, blocksize, fwd, st);
 }
 
 }  // extern "C"
