@@ -205,36 +205,71 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict
 // Single-pass decode with decoupled look-back (mc_scan.h): tiles numbered in
 // start order, the tile's aggregate published right after its block scan,
 // wave 0 walks back 64 predecessors per round.
-template <int D, int A>
+// COUNTER: tiles numbered by an atomic counter in start order (the counter
+// saturates at ~88 increments/us, MI355X_MICROARCH.md "dequeue").  Without
+// it the tile is blockIdx.x: with workgroups dispatched in increasing
+// blockIdx order per XCD the lowest-numbered waiting tile's predecessors are
+// all resident or done, so waits end; if a wait still exceeds the spin bound
+// the tile computes its prefix from the data itself, so the result is correct
+// under any dispatch order.
+template <int D, int A, bool COUNTER>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4_decode_lb(const uint8_t *__restrict__ src,
                                                           uint8_t *__restrict__ dst,
                                                           uint32_t *ctrl, uint64_t *status,
-                                                          C4Params p) {
+                                                          C4Params p, unsigned max_spins) {
   constexpr int DS = D == MC_F4 ? 4 : 8;
   __shared__ uint64_t red[MC_BLOCK / 64];
   __shared__ uint32_t slot;
   __shared__ uint32_t prefix_slot;
   __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
-  const size_t tile = mc_lb_tile(ctrl, &slot);
+  __shared__ int ok_slot;
+  const size_t tile = COUNTER ? mc_lb_tile(ctrl, &slot) : (size_t)blockIdx.x;
   uint32_t v[C4_PER], run;
   c4_local_scan<D, A>(src, tile, p, v, run);
   uint64_t agg;
   const uint32_t excl = (uint32_t)mc_block_excl_scan<false>(run, red, &agg);
   if (threadIdx.x < 64) {
-    const uint32_t pre = mc_lb_lookback_wave<false>(status, tile, (uint32_t)agg, ctrl + 1);
-    if (threadIdx.x == 0) prefix_slot = pre;
+    bool ok;
+    const uint32_t pre = mc_lb_lookback_wave<false>(status, tile, (uint32_t)agg, ok, max_spins);
+    if (threadIdx.x == 0) {
+      prefix_slot = pre;
+      ok_slot = ok;
+    }
   }
   __syncthreads();
+  if (!ok_slot) {
+    // a predecessor never published: sum every delta before this tile from
+    // the data itself (correct under any dispatch order), then publish
+    constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
+    uint32_t acc = 0;
+    for (size_t e = (size_t)threadIdx.x * C4_PER; e < tile * MC_SCAN_TILE; e += MC_BLOCK * C4_PER) {
+      uint32_t w[C4_PER];
+      load16_deltas<A, ES>(src, p.n, e, w);
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc += w[k];
+    }
+    uint64_t tot;
+    mc_block_excl_scan<false>(acc, red, &tot);
+    if (threadIdx.x == 0) {
+      prefix_slot = (uint32_t)tot;
+      mc_lb_publish_inclusive(status, tile, (uint32_t)tot + (uint32_t)agg);
+    }
+    __syncthreads();
+  }
   c4_finish<D, A>(dst, tile, v, prefix_slot + excl, outb, p);
 }
 
+// the workspace (tile counter + status words) is zeroed by the caller
 template <int D, int A>
-static void c4_decode_lb(const uint8_t *s, uint8_t *d, uint8_t *ws, const C4Params &p,
-                         hipStream_t st) {
+static void c4_decode_lb(const uint8_t *s, uint8_t *d, uint8_t *ws, const C4Params &p, bool counter,
+                         unsigned max_spins, hipStream_t st) {
   const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  hipMemsetAsync(ws, 0, mc_lb_workspace(ntiles), st);
-  k_c4_decode_lb<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(
-      s, d, reinterpret_cast<uint32_t *>(ws), reinterpret_cast<uint64_t *>(ws + 16), p);
+  if (counter)
+    k_c4_decode_lb<D, A, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(
+        s, d, reinterpret_cast<uint32_t *>(ws), reinterpret_cast<uint64_t *>(ws + 16), p, max_spins);
+  else
+    k_c4_decode_lb<D, A, false><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(
+        s, d, reinterpret_cast<uint32_t *>(ws), reinterpret_cast<uint64_t *>(ws + 16), p, max_spins);
 }
 
 template <int D, int A>
@@ -252,8 +287,9 @@ static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Para
   k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, sums, p);
 }
 
-// MCODEC_C4_VARIANT=2 selects the single-pass look-back decode (A/B
-// measurement; the three-pass decode is the default)
+// MCODEC_C4_VARIANT: 2 = single-pass look-back decode with an atomic tile
+// counter, 3 = look-back in blockIdx order, 4 = blockIdx order with the
+// data-derived fallback forced (tests); the default is chosen in DESIGN.md
 static int mc_c4_variant() {
   static int v = -1;
   if (v < 0) {
@@ -326,9 +362,17 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   hipStream_t st = (hipStream_t)stream;
-  if (n % 16 == 0 && mc_c4_variant() == 2) {
+  const int variant = mc_c4_variant();
+  if (n % 16 == 0 && (variant == 2 || variant == 3 || variant == 4)) {
     uint8_t *ws = static_cast<uint8_t *>(workspace);
-    MC_C4_DISPATCH(c4_decode_lb, s, d, ws, p, st);
+    const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+    const int rc = mc_hip_status(hipMemsetAsync(ws, 0, mc_lb_workspace(ntiles), st));
+    if (rc != MC_OK) return rc;
+    const bool counter = variant == 2;
+    // variant 4 (tests only): no waiting at all, every tile whose predecessor
+    // has not published yet takes the data-derived fallback
+    const unsigned spins = variant == 4 ? 0u : MC_LB_WAVE_SPINS;
+    MC_C4_DISPATCH(c4_decode_lb, s, d, ws, p, counter, spins, st);
   } else {
     uint64_t *sums = static_cast<uint64_t *>(workspace);
     MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);

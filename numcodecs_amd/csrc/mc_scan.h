@@ -149,12 +149,19 @@ MC_DEV uint32_t mc_lb_lookback(uint64_t *status_, size_t tile, uint32_t aggregat
 // Wave-parallel variant, called by ALL 64 lanes of ONE wave: each round reads
 // the status of 64 predecessors at once, so the walk back to the nearest
 // inclusive prefix takes distance/64 dependent round trips.  Returns the
-// exclusive prefix in every lane.
+// exclusive prefix in every lane and publishes the tile's inclusive prefix.
+// If a predecessor stays unpublished for MC_LB_WAVE_SPINS rounds, `ok` is set
+// false (wave-uniform) and nothing more is published: the caller then derives
+// the prefix from the data itself and publishes it (always correct, whatever
+// the dispatch order).
+constexpr unsigned MC_LB_WAVE_SPINS = 1u << 14;
+
 template <bool OR_OP>
-MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t aggregate,
-                                    uint32_t *error) {
+MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t aggregate, bool &ok,
+                                    unsigned max_spins = MC_LB_WAVE_SPINS) {
   mc_gu64 *status = (mc_gu64 *)status_;
   const int lane = threadIdx.x & 63;
+  ok = true;
   if (tile == 0) {
     if (lane == 0)
       __hip_atomic_store(&status[0], MC_LB_INC | aggregate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -171,9 +178,9 @@ MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t agg
     if (idx >= 0) s = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t flag = (uint32_t)(s >> 32);
     if (__any(flag == 0)) {
-      if (++spins > MC_LB_SPIN_LIMIT) {
-        if (lane == 0) __hip_atomic_store((mc_gu32 *)error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+      if (++spins > max_spins) {
+        ok = false;
+        return 0;
       }
       __builtin_amdgcn_s_sleep(1);
       continue;
@@ -195,6 +202,11 @@ MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t agg
     __hip_atomic_store(&status[tile], MC_LB_INC | incv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return prefix;
+}
+
+MC_DEV void mc_lb_publish_inclusive(uint64_t *status_, size_t tile, uint32_t inclusive) {
+  __hip_atomic_store(&((mc_gu64 *)status_)[tile], MC_LB_INC | inclusive, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // workspace layout for a look-back scan over ntiles tiles:
