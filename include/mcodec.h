@@ -265,6 +265,16 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize,
                     size_t blocksize, int mode, int forward, mc_stream_t stream);
 
 /* ---- tuning / measurement hooks (bench.py) ----------------------------- */
+/* mc_fso_delta_shuffle_decode with an explicit decode schedule: 0 default,
+ * 1 three-pass scan, 2 single-pass look-back with an atomic tile counter,
+ * 3 single-pass look-back in workgroup order, 4 = 3 with every wait replaced
+ * by the data-derived prefix fallback (for tests).  All give identical
+ * bytes. */
+int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n,
+                                        int astype, int dtype, double scale,
+                                        double offset, void *workspace,
+                                        size_t workspace_bytes, int variant,
+                                        mc_stream_t stream);
 /* Shuffle with an explicit kernel variant and grid (0 = default); used by
  * bench.py to sweep variants.  variant: 0 default, 1 register/dword stores,
  * 2 LDS-staged 16-B stores, 3 LDS both sides, 4 generic byte kernel. */

@@ -109,6 +109,9 @@ _SIGNATURES = {
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
     ],
     "mc_shuffle_variant": [_c_vp, _c_vp, _c_size, _c_size, _c_int, _c_int, _c_int, _c_vp],
+    "mc_fso_delta_shuffle_decode_variant": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_int, _c_vp,
+    ],
     "mc_checksum32_workspace": [_c_int, _c_size, _c_size],
     "mc_checksum32_batch": [
         _c_int, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp,

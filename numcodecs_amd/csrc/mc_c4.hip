@@ -290,6 +290,10 @@ static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Para
 // MCODEC_C4_VARIANT: 2 = single-pass look-back decode with an atomic tile
 // counter, 3 = look-back in blockIdx order, 4 = blockIdx order with the
 // data-derived fallback forced (tests); the default is chosen in DESIGN.md
+// decode variant used when neither the caller nor MCODEC_C4_VARIANT picks
+// one: 1 = three-pass scan (DESIGN.md records the A/B that chose it)
+constexpr int C4_DEFAULT_VARIANT = 1;
+
 static int mc_c4_variant() {
   static int v = -1;
   if (v < 0) {
@@ -349,11 +353,12 @@ size_t mc_fso_delta_shuffle_decode_workspace(size_t n) {
   return mc_lb_workspace(ntiles) > ntiles * 8 ? mc_lb_workspace(ntiles) : ntiles * 8;
 }
 
-int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype, int dtype,
-                                double scale, double offset, void *workspace,
-                                size_t workspace_bytes, mc_stream_t stream) {
+int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n, int astype, int dtype,
+                                        double scale, double offset, void *workspace,
+                                        size_t workspace_bytes, int variant, mc_stream_t stream) {
   if (n == 0) return MC_OK;
   if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
+  if (variant < 0 || variant > 4) return MC_EINVAL;
   if (!workspace || workspace_bytes < mc_fso_delta_shuffle_decode_workspace(n)) return MC_ENOSPC;
   C4Params p;
   p.n = n;
@@ -362,15 +367,15 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   hipStream_t st = (hipStream_t)stream;
-  const int variant = mc_c4_variant();
+  if (variant == 0) variant = mc_c4_variant() ? mc_c4_variant() : C4_DEFAULT_VARIANT;
   if (n % 16 == 0 && (variant == 2 || variant == 3 || variant == 4)) {
     uint8_t *ws = static_cast<uint8_t *>(workspace);
     const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
     const int rc = mc_hip_status(hipMemsetAsync(ws, 0, mc_lb_workspace(ntiles), st));
     if (rc != MC_OK) return rc;
     const bool counter = variant == 2;
-    // variant 4 (tests only): no waiting at all, every tile whose predecessor
-    // has not published yet takes the data-derived fallback
+    // variant 4 (tests): no waiting at all, every tile whose predecessor has
+    // not published yet takes the data-derived fallback
     const unsigned spins = variant == 4 ? 0u : MC_LB_WAVE_SPINS;
     MC_C4_DISPATCH(c4_decode_lb, s, d, ws, p, counter, spins, st);
   } else {
@@ -378,6 +383,13 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype
     MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
   }
   return mc_last_launch();
+}
+
+int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype, int dtype,
+                                double scale, double offset, void *workspace,
+                                size_t workspace_bytes, mc_stream_t stream) {
+  return mc_fso_delta_shuffle_decode_variant(src, dst, n, astype, dtype, scale, offset, workspace,
+                                             workspace_bytes, 0, stream);
 }
 
 }  // extern "C"

@@ -46,32 +46,71 @@ MC_DEV uint64_t mc_block_excl_scan(uint64_t v, uint64_t *lds, uint64_t *total) {
   return mc_scan_combine<OR_OP>(wpre, lane ? excl_in_wave : 0);
 }
 
-// Exclusive scan of `ntiles` tile totals in place, one workgroup of 1024:
-// each thread keeps 16 consecutive totals in registers (all loads in flight
-// at once), one block scan per round of 16384 totals.
+// Exclusive scan of `ntiles` tile totals in place, one workgroup of 1024
+// (tools/scan_bench.hip measures it alone).  Per round of 8192 totals each
+// wave moves its 512 through an LDS slice with coalesced global accesses
+// (lane l loads l + 64k) and scans them as 8 consecutive totals per lane
+// (serial adds), so one block scan -- one wave scan per wave -- is all the
+// cross-lane work.  Two layouts measured slower: 16 consecutive totals per
+// lane straight from global (each load instruction touches 64 cache lines on
+// one CU: 18.7 us for 16K totals), 64-lane columns scanned across the wave
+// (16 wave scans of 64-bit shuffles per round: 15.5 us) and 16K-total rounds
+// (a 128 KiB LDS workgroup adds ~4 us of fixed cost).  This one: 9.2 us for
+// 16K totals, 4.8 us for one round, the next round's loads issued early.
 template <bool OR_OP>
 __global__ __launch_bounds__(1024) void k_scan_sums(uint64_t *__restrict__ sums, size_t ntiles) {
-  constexpr int PER = 16, ROUND = 1024 * PER;
+  constexpr int PER = 8, WSPAN = 64 * PER, ROUND = 1024 * PER;  // 64 KiB LDS
   __shared__ uint64_t red[1024 / 64];
+  __shared__ __attribute__((aligned(16))) uint64_t buf[ROUND];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t *wbuf = buf + wave * WSPAN;
   uint64_t carry = 0;
+  const size_t last = ntiles - 1;
+  uint64_t x[PER];  // this round's totals; the next round's are loaded early
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const size_t i = (size_t)wave * WSPAN + lane + 64 * k;
+    x[k] = sums[i < last ? i : last];
+  }
   for (size_t r0 = 0; r0 < ntiles; r0 += ROUND) {
-    const size_t i0 = r0 + (size_t)threadIdx.x * PER;
+    const size_t wb = r0 + (size_t)wave * WSPAN + lane;
+    uint64_t xn[PER];
+    if (r0 + ROUND < ntiles) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const size_t i = wb + ROUND + 64 * k;
+        xn[k] = sums[i < last ? i : last];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) wbuf[lane + 64 * k] = wb + 64 * k < ntiles ? x[k] : 0;
+    // the wave reads back what it wrote: no barrier needed, only LDS ordering
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
     uint64_t v[PER];
 #pragma unroll
-    for (int j = 0; j < PER; ++j) v[j] = i0 + j < ntiles ? sums[i0 + j] : 0;
+    for (int k = 0; k < PER; ++k) v[k] = wbuf[PER * lane + k];
     uint64_t run = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint64_t x = v[j];
-      v[j] = run;
-      run = mc_scan_combine<OR_OP>(run, x);
+    for (int k = 0; k < PER; ++k) {
+      const uint64_t t = v[k];
+      v[k] = run;
+      run = mc_scan_combine<OR_OP>(run, t);
     }
     uint64_t tot;
     const uint64_t excl = mc_scan_combine<OR_OP>(carry, mc_block_excl_scan<OR_OP>(run, red, &tot));
 #pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if (i0 + j < ntiles) sums[i0 + j] = mc_scan_combine<OR_OP>(excl, v[j]);
+    for (int k = 0; k < PER; ++k) wbuf[PER * lane + k] = mc_scan_combine<OR_OP>(excl, v[k]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (wb + 64 * k < ntiles) sums[wb + 64 * k] = wbuf[lane + 64 * k];
     carry = mc_scan_combine<OR_OP>(carry, tot);
+    if (r0 + ROUND < ntiles) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) x[k] = xn[k];
+    }
   }
 }
 
