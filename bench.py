@@ -345,6 +345,24 @@ def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
     res["pcie_h2d_GiBps"] = round(total_gib / h2d, 2)
     res["pcie_d2h_GiBps"] = round(total_gib / d2h, 2)
     res["workload"] = f"{total_gib} GiB of {chunk_bytes // MiB} MiB chunks in pinned host memory, Shuffle(4), host->host"
+    # a Zarr filter chain streamed host -> host (numcodecs_amd.chunks)
+    from numcodecs_amd import CRC32, BitRound, Shuffle, chunks
+
+    codecs = [BitRound(10), Shuffle(4), CRC32()]
+    x32 = hin.view(torch.float32)
+    x32.copy_(torch.randn(x32.shape))
+    chunks.host_encode_chunks(codecs, x32, henc_z := torch.empty((nchunks, chunk_bytes + 4), dtype=torch.uint8).pin_memory())
+    t0 = time.perf_counter()
+    chunks.host_encode_chunks(codecs, x32, henc_z)
+    te = time.perf_counter() - t0
+    out = hdec.view(torch.float32)
+    t0 = time.perf_counter()
+    chunks.host_decode_chunks(codecs, henc_z, out)
+    td = time.perf_counter() - t0
+    res["zarr_chain_bitround10_shuffle4_crc32"] = {
+        "encode_GiBps": round(nchunks * chunk_bytes / GiB / te, 2),
+        "decode_GiBps": round(nchunks * chunk_bytes / GiB / td, 2),
+    }
     return res
 
 

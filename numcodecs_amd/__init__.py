@@ -57,7 +57,8 @@ from .packbits import PackBits
 register_codec(PackBits)
 
 from . import batch  # noqa: E402,F401
-from . import blosc_shuffle  # noqa: E402,F401  (Blosc's per-block shuffle filters)  (batched chunk API and fused pipelines)
+from . import blosc_shuffle  # noqa: E402,F401  (Blosc's per-block shuffle filters)
+from . import chunks  # noqa: E402,F401  (Zarr-style batched / host-streamed chunk pipelines)  (batched chunk API and fused pipelines)
 
 __version__ = "0.1.0"
 
@@ -78,6 +79,7 @@ __all__ = [
     "UnknownCodecError",
     "batch",
     "blosc_shuffle",
+    "chunks",
     "codec_registry",
     "get_codec",
     "register_codec",
