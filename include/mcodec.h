@@ -120,6 +120,18 @@ size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
                     int dtype, void *workspace, size_t workspace_bytes,
                     mc_stream_t stream);
+/* Batched Delta over nchunks chunks of n elements each (chunk c read at
+ * src + c*src_stride, written at dst + c*dst_stride; strides in bytes).
+ * Each chunk is an independent Delta (its own first element / cumsum).
+ * Decode runs one workgroup per chunk (integer: single-pass scan with a
+ * running carry; float: one sequential add chain per chunk) and needs no
+ * workspace. */
+int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst,
+                          size_t dst_stride, size_t nchunks, size_t n,
+                          int dtype, int astype, mc_stream_t stream);
+int mc_delta_decode_batch(const void *src, size_t src_stride, void *dst,
+                          size_t dst_stride, size_t nchunks, size_t n,
+                          int astype, int dtype, mc_stream_t stream);
 
 /* ---- FixedScaleOffset / Quantize / casts ------------------------------ */
 /* Scalars arrive already converted (on the host, by numpy's NEP 50 rules) to
@@ -275,6 +287,14 @@ int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n,
                                         double offset, void *workspace,
                                         size_t workspace_bytes, int variant,
                                         mc_stream_t stream);
+/* mc_delta_decode_batch with an explicit float-chain schedule (LDS slot
+ * bytes / chain values per LDS read group): 0 default (by batch size),
+ * 1 32 KiB/16, 2 32 KiB/32, 3 8 KiB/16, 4 8 KiB/32, 5 4 KiB/32.  Integer
+ * dtypes ignore it.  All give identical bytes. */
+int mc_delta_decode_batch_variant(const void *src, size_t src_stride,
+                                  void *dst, size_t dst_stride,
+                                  size_t nchunks, size_t n, int astype,
+                                  int dtype, int variant, mc_stream_t stream);
 /* Shuffle with an explicit kernel variant and grid (0 = default); used by
  * bench.py to sweep variants.  variant: 0 default, 1 register/dword stores,
  * 2 LDS-staged 16-B stores, 3 LDS both sides, 4 generic byte kernel. */

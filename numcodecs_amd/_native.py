@@ -81,6 +81,10 @@ _SIGNATURES = {
     "mc_delta_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_workspace": [_c_size, _c_int, _c_int],
     "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
+    "mc_delta_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
+    "mc_delta_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
+    "mc_delta_decode_batch_variant": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_int,
+                                      _c_vp],
     "mc_fso_encode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int,
         _c_double, _c_i64, _c_double, _c_i64, _c_vp,

@@ -87,6 +87,23 @@ def delta_encode(src, dst, n, dtype, astype) -> None:
                                   dtype_code(astype), stream(src)), "mc_delta_encode")
 
 
+def delta_batch(src, src_stride, dst, dst_stride, nchunks, n, dtype, astype, encode) -> None:
+    """Delta encode (dtype -> astype) or decode (astype -> dtype) of nchunks
+    chunks of n elements each (byte strides)."""
+    _native.require_device()
+    if n == 0 or nchunks == 0:
+        return
+    with _guard(src):
+        if encode:
+            check(lib.mc_delta_encode_batch(src.data_ptr(), src_stride, dst.data_ptr(), dst_stride, nchunks, n,
+                                            dtype_code(dtype), dtype_code(astype), stream(src)),
+                  "mc_delta_encode_batch")
+        else:
+            check(lib.mc_delta_decode_batch(src.data_ptr(), src_stride, dst.data_ptr(), dst_stride, nchunks, n,
+                                            dtype_code(astype), dtype_code(dtype), stream(src)),
+                  "mc_delta_decode_batch")
+
+
 def delta_decode(src, dst, n, astype, dtype) -> None:
     _native.require_device()
     if n == 0:

@@ -26,7 +26,7 @@ from . import _native, _ops
 from ._native import check, lib
 from .bitround import BitRound, max_bits
 from .compat import ensure_contiguous_ndarray, is_device_tensor
-from .delta import Delta
+from .delta import Delta, check_first_elements
 from .fixedscaleoffset import FixedScaleOffset, _resolve
 from .fletcher32 import Fletcher32, _mismatch
 from .shuffle import Shuffle
@@ -89,6 +89,32 @@ def unshuffle_chunks(chunks, elementsize, out=None):
     out = torch.empty((b, n), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
     if b and n:
         _ops.shuffle_batch(rows, rows.stride(0), out, out.stride(0), b, n, elementsize, False)
+    return out
+
+
+def delta_chunks(chunks, delta, encode=True, out=None):
+    """Delta(dtype, astype).encode (or .decode) of every chunk of a [B, ...]
+    device batch, each chunk independently (its own first element / running
+    sum), in one launch; returns [B, m] uint8 rows.  Rows are the chunks' raw
+    bytes (dtype elements for encode, astype elements for decode)."""
+    rows = _as_rows(chunks)
+    b, nb = rows.shape
+    src_t, dst_t = (delta.dtype, delta.astype) if encode else (delta.astype, delta.dtype)
+    if nb % src_t.itemsize:
+        raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
+    n = nb // src_t.itemsize
+    if encode and n == 0 and b:
+        raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+    if encode and b:
+        check_first_elements(rows[:, : src_t.itemsize], delta.dtype, delta.astype)
+    if not encode and not np.can_cast(delta.astype, delta.dtype, casting="same_kind"):
+        raise TypeError(
+            f"Cannot cast ufunc 'add' output from {delta.astype!r} to {delta.dtype!r} with casting rule 'same_kind'"
+        )
+    m = n * dst_t.itemsize
+    out = torch.empty((b, m), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if b and n:
+        _ops.delta_batch(rows, rows.stride(0), out, out.stride(0), b, n, delta.dtype, delta.astype, encode)
     return out
 
 

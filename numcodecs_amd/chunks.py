@@ -10,7 +10,8 @@ offers the same result for a whole batch:
   of a device batch ``[B, ...]``.  Each step runs batched where its kernel
   allows: elementwise codecs (BitRound, Quantize, FixedScaleOffset, AsType)
   on the flattened batch in one launch, Shuffle and the checksums as batch
-  launches; Delta and PackBits (whose chunk boundaries matter) row by row.
+  launches, Delta as a batch launch with one scan per chunk; PackBits
+  (whose chunk boundaries and header matter) row by row.
 * :func:`host_encode_chunks` / :func:`host_decode_chunks` stream host
   chunks through that chain: slices flow through a ring of device buffers on
   three role streams (H2D / kernels / D2H), so both PCIe directions and the
@@ -30,6 +31,7 @@ from .astype import AsType
 from .bitround import BitRound
 from .checksum32 import CRC32, CRC32C, Adler32, JenkinsLookup3
 from .compat import is_device_tensor
+from .delta import Delta
 from .fixedscaleoffset import FixedScaleOffset
 from .fletcher32 import Fletcher32, _mismatch
 from .quantize import Quantize
@@ -112,6 +114,8 @@ def _encode_step(c, x: torch.Tensor) -> torch.Tensor:
         return batch.checksum32_encode_chunks(rows, "jenkins_lookup3", value=c.initval, prefix=c.prefix)
     if isinstance(c, Fletcher32):
         return _fletcher32_encode_rows(rows)
+    if isinstance(c, Delta):
+        return batch.delta_chunks(rows, c, encode=True)
     return _per_row(c.encode, x)
 
 
@@ -145,6 +149,8 @@ def _decode_step(c, x: torch.Tensor, pending=None) -> torch.Tensor:
         return _checksum32_decode_rows(c, rows, pending)
     if isinstance(c, Fletcher32):
         return _fletcher32_decode_rows(rows, pending)
+    if isinstance(c, Delta):
+        return batch.delta_chunks(rows, c, encode=False)
     return _per_row(c.decode, x)
 
 

@@ -149,7 +149,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitround(const uint8_t *__restrict
 template <int D_, int A_, bool VEC>
 __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc(const uint8_t *__restrict__ src,
                                                         uint8_t *__restrict__ dst, size_t n,
-                                                        int d_rt, int a_rt) {
+                                                        int d_rt, int a_rt, size_t src_stride,
+                                                        size_t dst_stride) {
+  src += (size_t)blockIdx.y * src_stride;  // chunk blockIdx.y of a batch
+  dst += (size_t)blockIdx.y * dst_stride;
   const int d = D_ >= 0 ? D_ : d_rt;
   const int a = A_ >= 0 ? A_ : a_rt;
   const int ss = mc_itemsize(d), ds = mc_itemsize(a);
@@ -294,20 +297,33 @@ int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, dou
 
 int mc_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype,
                     mc_stream_t stream) {
+  return mc_delta_encode_batch(src, 0, dst, 0, 1, n, dtype, astype, stream);
+}
+
+int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                          size_t nchunks, size_t n, int dtype, int astype, mc_stream_t stream) {
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
-  if (n == 0) return MC_OK;
+  if (n == 0 || nchunks == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;
+  const int ss = mc_itemsize(dtype), ds = mc_itemsize(astype);
+  if (nchunks > 1 && (src_stride < n * ss || dst_stride < n * ds)) return MC_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
-  const bool vec = aligned_for(src, mc_itemsize(dtype)) && aligned_for(dst, mc_itemsize(astype));
-  const unsigned grid = blocks_for(n);
-  if (vec && dtype == MC_I2 && astype == MC_I2)
-    k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
-  else if (vec)
-    k_delta_enc<-1, -1, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
-  else
-    k_delta_enc<-1, -1, false><<<grid, MC_BLOCK, 0, st>>>(s, d, n, dtype, astype);
+  const bool vec = aligned_for(src, ss) && aligned_for(dst, ds) &&
+                   (nchunks == 1 || (src_stride % (4 * ss) == 0 && dst_stride % (4 * ds) == 0));
+  constexpr size_t YMAX = 65535;
+  for (size_t c0 = 0; c0 < nchunks; c0 += YMAX) {
+    const dim3 grid(blocks_for(n), (unsigned)min(YMAX, nchunks - c0));
+    const uint8_t *sc = s + c0 * src_stride;
+    uint8_t *dc = d + c0 * dst_stride;
+    if (vec && dtype == MC_I2 && astype == MC_I2)
+      k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
+    else if (vec)
+      k_delta_enc<-1, -1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
+    else
+      k_delta_enc<-1, -1, false><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
+  }
   return mc_last_launch();
 }
 

@@ -11,9 +11,12 @@
 //   * bool: numpy's bool add loop is logical or -- also associative.
 //   * float dtypes: numpy adds left to right with a rounding after every add;
 //     no reassociation reproduces that, so the float path keeps the serial
-//     order exactly: one wave streams 1024-element blocks into LDS with
-//     coalesced loads and lane 0 runs the dependent adds.  Bit-exact, not fast
-//     (the integer-Delta pipeline is the bench path).
+//     order exactly (k_scan_serial: one dependent add chain per chunk fed
+//     through double-buffered LDS by a second wave).  Bit-exact; a single
+//     chunk runs at the latency of one add per element, batches
+//     run one chain per workgroup.
+//   * batches of chunks (mc_delta_decode_batch): one workgroup per chunk with
+//     a running carry (k_scan_rows), single pass.
 #include "mc_scan.h"
 
 namespace {
@@ -102,31 +105,285 @@ __global__ __launch_bounds__(MC_BLOCK) void k_scan_apply(const uint8_t *__restri
   }
 }
 
-// float dtypes: exact left-to-right accumulation (one wave)
-constexpr int SER_BLK = 1024;
+// ---------------------------------------------------------------------------
+// float dtypes: exact left-to-right accumulation, one workgroup per chunk.
+// numpy's add.accumulate rounds after every add in order, so the adds form
+// one dependent chain per chunk.  Two waves: lane 0 of wave 0 runs the chain
+// over a block held in LDS (8 values per ds_read/ds_write group, only the add
+// itself on the critical path) while wave 1 stores the previous block's
+// results and loads + converts the next one into the other LDS slot with
+// coalesced vector accesses, so HBM latency and the dtype conversions hide
+// behind the chain.  A batch of chunks runs one chain per workgroup.
+// ---------------------------------------------------------------------------
+template <int D> struct SerAcc { using T = float; };
+template <> struct SerAcc<MC_F8> { using T = double; };
 
-__global__ __launch_bounds__(64) void k_scan_serial(const uint8_t *__restrict__ src,
-                                                    uint8_t *__restrict__ dst, size_t n, int a,
-                                                    int d) {
-  __shared__ uint64_t buf[SER_BLK];
-  const int as = mc_itemsize(a), ds = mc_itemsize(d);
-  const int lane = threadIdx.x;
-  McNum acc = mc_num_f(0.0);
-  for (size_t b0 = 0; b0 < n; b0 += SER_BLK) {
-    const size_t cnt = min((size_t)SER_BLK, n - b0);
-    for (int j = lane; j < (int)cnt; j += 64) buf[j] = mc_load_elem_u(src, b0 + j, as);
-    __syncthreads();
-    if (lane == 0) {
-      for (int j = 0; j < (int)cnt; ++j) {
-        const McNum x = mc_num_cast(mc_num_from_bits(buf[j], a), a, d);
-        acc = (b0 + j == 0) ? x : mc_num_binop(acc, x, MC_OP_ADD, d);
-        buf[j] = mc_num_to_bits(acc, d);
+template <int D>
+MC_DEV typename SerAcc<D>::T ser_add(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
+  if constexpr (D == MC_F2) {
+    // numpy's half loop: float32 add, then npy_float_to_half.  The hardware
+    // RNE conversion (denormals kept) gives the same half for every non-NaN
+    // sum; NaN sums take numpy's payload-preserving routine.
+    const float r = a + b;
+    if (__builtin_isnan(r)) return mc_half_to_float(mc_float_to_half(r));
+    return (float)(_Float16)r;
+  } else {
+    return a + b;
+  }
+}
+
+// G chain values as 16-B LDS accesses (p 16-B aligned)
+template <typename T, int SER_G>
+MC_DEV void ser_ld(const T *p, T (&r)[SER_G]) {
+  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int W = 16 / sizeof(T);
+#pragma unroll
+  for (int v = 0; v < SER_G / W; ++v) {
+    const vec x = reinterpret_cast<const vec *>(p)[v];
+#pragma unroll
+    for (int e = 0; e < W; ++e) r[v * W + e] = x[e];
+  }
+}
+template <typename T, int SER_G>
+MC_DEV void ser_st(T *p, const T (&r)[SER_G]) {
+  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int W = 16 / sizeof(T);
+#pragma unroll
+  for (int v = 0; v < SER_G / W; ++v) {
+    vec x;
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = r[v * W + e];
+    reinterpret_cast<vec *>(p)[v] = x;
+  }
+}
+
+constexpr int SER_UN = 8;              // vectors of 4 elements in flight per lane
+
+template <int A_, int D, bool VEC, int SER_SLOT_BYTES = 32768, int SER_G = 16>
+__global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__ src,
+                                                     size_t src_stride,
+                                                     uint8_t *__restrict__ dst,
+                                                     size_t dst_stride, size_t n, int a_rt) {
+  using T = typename SerAcc<D>::T;
+  constexpr int BLK = SER_SLOT_BYTES / (int)sizeof(T);
+  constexpr int DS = D == MC_F8 ? 8 : (D == MC_F4 ? 4 : 2);
+  __shared__ __attribute__((aligned(16))) T slot[2][BLK + 2 * SER_G];
+  const int a = A_ >= 0 ? A_ : a_rt;
+  const int as = mc_itemsize(a);
+  src += (size_t)blockIdx.x * src_stride;
+  dst += (size_t)blockIdx.x * dst_stride;
+  const int lane = threadIdx.x & 63;
+  const bool io = threadIdx.x >= 64;
+  const size_t nb = (n + BLK - 1) / BLK;
+
+  auto to_acc = [&](uint64_t bits) -> T {
+    return (T)mc_num_cast(mc_num_from_bits(bits, a), a, D).f;
+  };
+  auto load_blk = [&](size_t b) {  // wave 1: src block b -> slot[b & 1]
+    const size_t b0 = b * BLK;
+    const int cnt = (int)min((size_t)BLK, n - b0);
+    T *p = slot[b & 1];
+    for (int r0 = 0; r0 < cnt; r0 += 4 * 64 * SER_UN) {
+      uint64_t e[SER_UN][4];
+#pragma unroll
+      for (int u = 0; u < SER_UN; ++u) {
+        const int j = r0 + 4 * (u * 64 + lane);
+        if (VEC && j + 4 <= cnt) {
+          mc_load4(src + (b0 + j) * as, as, e[u]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            e[u][k] = j + k < cnt ? mc_load_elem_u(src, b0 + j + k, as) : 0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SER_UN; ++u) {
+        const int j = r0 + 4 * (u * 64 + lane);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (j + k < cnt) p[j + k] = to_acc(e[u][k]);
+      }
+    }
+  };
+  auto store_blk = [&](size_t b) {  // wave 1: slot[b & 1] -> dst block b
+    const size_t b0 = b * BLK;
+    const int cnt = (int)min((size_t)BLK, n - b0);
+    const T *p = slot[b & 1];
+    for (int j = 4 * lane; j < cnt; j += 4 * 64) {
+      uint64_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = j + k < cnt ? mc_num_to_bits(mc_num_f((double)p[j + k]), D) : 0;
+      if (VEC && j + 4 <= cnt) {
+        mc_store4(dst + (b0 + j) * DS, DS, o);
+      } else {
+        for (int k = 0; k < 4 && j + k < cnt; ++k) mc_store_elem_u(dst, b0 + j + k, DS, o[k]);
+      }
+    }
+  };
+
+  if (io) load_blk(0);
+  __syncthreads();
+  T acc = 0;
+  for (size_t b = 0; b < nb; ++b) {
+    if (io) {
+      if (b >= 1) store_blk(b - 1);
+      if (b + 1 < nb) load_blk(b + 1);
+    } else if (lane == 0) {
+      // software-pipelined chain: group g+1's LDS reads are in flight while
+      // group g's adds run (ds_read latency ~50 cycles vs ~G dependent adds)
+      T *p = slot[b & 1];
+      const int cnt = (int)min((size_t)BLK, n - b * BLK);
+      int j = 0;
+      if (b == 0) {  // out[0] = x[0] exactly (no add), then align to a group
+        acc = p[0];
+        const int m = cnt < SER_G ? cnt : SER_G;
+        for (int k = 1; k < m; ++k) {
+          acc = ser_add<D>(acc, p[k]);
+          p[k] = acc;
+        }
+        j = m;
+      }
+      // two register groups alternate: while one group's adds run, the other
+      // group's 16-B LDS reads are in flight (the slot is padded by 2 groups,
+      // so the read-ahead never leaves it)
+      if (j + 2 * SER_G <= cnt) {
+        T ga[SER_G], gb[SER_G];
+        ser_ld<T, SER_G>(p + j, ga);
+        for (; j + 2 * SER_G <= cnt; j += 2 * SER_G) {
+          ser_ld<T, SER_G>(p + j + SER_G, gb);
+          __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead ahead of the adds
+#pragma unroll
+          for (int k = 0; k < SER_G; ++k) {
+            acc = ser_add<D>(acc, ga[k]);
+            ga[k] = acc;
+          }
+          ser_st<T, SER_G>(p + j, ga);
+          ser_ld<T, SER_G>(p + j + 2 * SER_G, ga);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < SER_G; ++k) {
+            acc = ser_add<D>(acc, gb[k]);
+            gb[k] = acc;
+          }
+          ser_st<T, SER_G>(p + j + SER_G, gb);
+        }
+      }
+      for (; j < cnt; ++j) {
+        acc = ser_add<D>(acc, p[j]);
+        p[j] = acc;
       }
     }
     __syncthreads();
-    for (int j = lane; j < (int)cnt; j += 64) mc_store_elem_u(dst, b0 + j, ds, buf[j]);
-    __syncthreads();
   }
+  if (io) store_blk(nb - 1);
+}
+
+// (slot bytes, group) per schedule: a 32 KiB slot amortises the block
+// barrier for one long chain; a batch needs small slots so that many chains
+// (workgroups) fit a CU's LDS at once (2 x 32 KiB slots allow only 2).
+template <int D>
+static void launch_serial(const uint8_t *s, size_t ss, uint8_t *d, size_t dss, size_t n,
+                          size_t rows, int a, hipStream_t st, int variant = 0) {
+  const int as = mc_itemsize(a);
+  const bool vec = ((uintptr_t)s % (4 * as) == 0) && (ss % (4 * as) == 0) &&
+                   ((uintptr_t)d % (4 * mc_itemsize(D)) == 0) && (dss % (4 * mc_itemsize(D)) == 0);
+  // measured (tools/probe_delta.py, profiles/r01/probe_delta.json): one chain
+  // 32 KiB / 32; 2048 chains of 1 MiB 8 KiB slots, 32-value groups for f4
+  // and 16 for f8
+  if (variant == 0) variant = rows >= 256 ? (D == MC_F8 ? 3 : 4) : 2;
+  const unsigned g = (unsigned)rows;
+  if (vec && a == D) {
+    switch (variant) {
+      case 1: k_scan_serial<D, D, true, 32768, 16><<<g, 128, 0, st>>>(s, ss, d, dss, n, a); break;
+      case 2: k_scan_serial<D, D, true, 32768, 32><<<g, 128, 0, st>>>(s, ss, d, dss, n, a); break;
+      case 3: k_scan_serial<D, D, true, 8192, 16><<<g, 128, 0, st>>>(s, ss, d, dss, n, a); break;
+      case 4: k_scan_serial<D, D, true, 8192, 32><<<g, 128, 0, st>>>(s, ss, d, dss, n, a); break;
+      default: k_scan_serial<D, D, true, 4096, 32><<<g, 128, 0, st>>>(s, ss, d, dss, n, a); break;
+    }
+  } else if (vec) {
+    k_scan_serial<-1, D, true, 8192, 16><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+  } else {
+    k_scan_serial<-1, D, false, 8192, 16><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+  }
+}
+
+static void launch_serial_any(const uint8_t *s, size_t ss, uint8_t *d, size_t dss, size_t n,
+                              size_t rows, int a, int dt, hipStream_t st, int variant = 0) {
+  if (dt == MC_F8) launch_serial<MC_F8>(s, ss, d, dss, n, rows, a, st, variant);
+  else if (dt == MC_F4) launch_serial<MC_F4>(s, ss, d, dss, n, rows, a, st, variant);
+  else launch_serial<MC_F2>(s, ss, d, dss, n, rows, a, st, variant);
+}
+
+// ---------------------------------------------------------------------------
+// integer / bool Delta decode of a batch of chunks: one workgroup per chunk
+// walks its chunk in 4096-element tiles with a running carry (single pass,
+// no workspace).  The next tile's loads are issued before the current tile's
+// block scans, so each workgroup keeps 2 tiles of reads in flight; thousands
+// of chunks fill the chip.  (A single large chunk uses the 3-pass scan.)
+// ---------------------------------------------------------------------------
+template <bool OR_OP, int A_, int D_, bool VEC>
+__global__ __launch_bounds__(MC_BLOCK) void k_scan_rows(const uint8_t *__restrict__ src,
+                                                        size_t src_stride,
+                                                        uint8_t *__restrict__ dst,
+                                                        size_t dst_stride, size_t n, int a_rt,
+                                                        int d_rt) {
+  __shared__ uint64_t lds[MC_BLOCK / 64];
+  const int a = A_ >= 0 ? A_ : a_rt, d = D_ >= 0 ? D_ : d_rt;
+  const int ds = mc_itemsize(d);
+  src += (size_t)blockIdx.x * src_stride;
+  dst += (size_t)blockIdx.x * dst_stride;
+  uint64_t carry = 0;
+  uint64_t v[MC_SCAN_STEPS][4];
+  int cnt[MC_SCAN_STEPS];
+  auto load_tile = [&](size_t base) {
+#pragma unroll
+    for (int s = 0; s < MC_SCAN_STEPS; ++s)
+      load4_acc<A_, D_, VEC>(src, base + (size_t)s * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x, n, a,
+                             d, v[s], cnt[s]);
+  };
+  if (n) load_tile(0);
+  for (size_t base = 0; base < n; base += MC_SCAN_TILE) {
+    uint64_t cur[MC_SCAN_STEPS][4];
+    int ccnt[MC_SCAN_STEPS];
+#pragma unroll
+    for (int s = 0; s < MC_SCAN_STEPS; ++s) {
+      ccnt[s] = cnt[s];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[s][k] = v[s][k];
+    }
+    if (base + MC_SCAN_TILE < n) load_tile(base + MC_SCAN_TILE);
+#pragma unroll
+    for (int s = 0; s < MC_SCAN_STEPS; ++s) {
+      const size_t i0 = base + (size_t)s * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
+      uint64_t p[4];
+      uint64_t run = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        run = mc_scan_combine<OR_OP>(run, cur[s][k]);
+        p[k] = run;
+      }
+      uint64_t tot;
+      const uint64_t excl = mc_block_excl_scan<OR_OP>(run, lds, &tot);
+      const uint64_t pre = mc_scan_combine<OR_OP>(carry, excl);
+      uint64_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = (uint64_t)mc_wrap((int64_t)mc_scan_combine<OR_OP>(pre, p[k]), d);
+      if (VEC && ccnt[s] == 4) {
+        mc_store4(dst + i0 * ds, ds, o);
+      } else {
+        for (int k = 0; k < ccnt[s]; ++k) mc_store_elem_u(dst, i0 + k, ds, o[k]);
+      }
+      carry = mc_scan_combine<OR_OP>(carry, tot);
+    }
+  }
+}
+
+template <bool OR_OP, int A_, int D_, bool VEC>
+static void launch_rows(const uint8_t *s, size_t ss, uint8_t *d, size_t dss, size_t n, size_t rows,
+                        int a, int dt, hipStream_t st) {
+  k_scan_rows<OR_OP, A_, D_, VEC><<<(unsigned)rows, MC_BLOCK, 0, st>>>(s, ss, d, dss, n, a, dt);
 }
 
 template <bool OR_OP, int A_, int D_, bool VEC>
@@ -156,7 +413,7 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   if (mc_is_float(dtype)) {
-    k_scan_serial<<<1, 64, 0, st>>>(s, d, n, astype, dtype);
+    launch_serial_any(s, 0, d, 0, n, 1, astype, dtype, st);
     return mc_last_launch();
   }
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
@@ -175,6 +432,52 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
     launch_int_scan<false, -1, -1, true>(s, d, n, astype, dtype, sums, ntiles, st);
   } else {
     launch_int_scan<false, -1, -1, false>(s, d, n, astype, dtype, sums, ntiles, st);
+  }
+  return mc_last_launch();
+}
+
+int mc_delta_decode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                          size_t nchunks, size_t n, int astype, int dtype, mc_stream_t stream) {
+  return mc_delta_decode_batch_variant(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype,
+                                       0, stream);
+}
+
+int mc_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst,
+                                  size_t dst_stride, size_t nchunks, size_t n, int astype,
+                                  int dtype, int variant, mc_stream_t stream) {
+  if (variant < 0 || variant > 5) return MC_EINVAL;
+  if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
+  if (n == 0 || nchunks == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < n * mc_itemsize(astype) || dst_stride < n * mc_itemsize(dtype)))
+    return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  constexpr size_t GRID_MAX = 1u << 30;
+  for (size_t c0 = 0; c0 < nchunks; c0 += GRID_MAX) {
+    const size_t rows = min(GRID_MAX, nchunks - c0);
+    const uint8_t *sc = s + c0 * src_stride;
+    uint8_t *dc = d + c0 * dst_stride;
+    if (mc_is_float(dtype)) {
+      launch_serial_any(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st, variant);
+      continue;
+    }
+    const size_t as = mc_itemsize(astype), ds = mc_itemsize(dtype);
+    const bool vec = ((uintptr_t)sc % (4 * as) == 0) && (src_stride % (4 * as) == 0) &&
+                     ((uintptr_t)dc % (4 * ds) == 0) && (dst_stride % (4 * ds) == 0);
+    if (dtype == MC_B1) {
+      if (vec) launch_rows<true, -1, -1, true>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+      else launch_rows<true, -1, -1, false>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+    } else if (vec && astype == MC_I2 && dtype == MC_I2) {
+      launch_rows<false, MC_I2, MC_I2, true>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+    } else if (vec && astype == MC_I4 && dtype == MC_I4) {
+      launch_rows<false, MC_I4, MC_I4, true>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+    } else if (vec) {
+      launch_rows<false, -1, -1, true>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+    } else {
+      launch_rows<false, -1, -1, false>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
+    }
   }
   return mc_last_launch();
 }

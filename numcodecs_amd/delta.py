@@ -16,6 +16,20 @@ from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
 __all__ = ["Delta"]
 
 
+def check_first_elements(firsts, dtype, astype) -> None:
+    """delta.py:63 writes ``enc[0] = arr[0]``: a numpy scalar assignment,
+    which raises OverflowError (ValueError for NaN) or warns when the first
+    element does not fit `astype`, unlike the array cast of the differences.
+    Replayed on the host with numpy itself, for casts that are not safe only.
+    `firsts` is a device uint8 tensor [..., itemsize] holding first elements."""
+    if np.can_cast(dtype, astype, casting="safe"):
+        return
+    vals = np.frombuffer(firsts.reshape(-1).cpu().numpy().tobytes(), dtype=dtype)
+    tmp = np.empty(1, dtype=astype)
+    for v in vals:
+        tmp[0] = v
+
+
 class Delta(Codec):
     """Codec to encode data as the difference between adjacent values.
 
@@ -57,6 +71,7 @@ class Delta(Codec):
         n = src.nbytes // self.dtype.itemsize
         if n == 0:  # enc[0] = arr[0] on an empty array (delta.py:63)
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        check_first_elements(src.data[: self.dtype.itemsize], self.dtype, self.astype)
         dst = empty_like_bytes(n * self.astype.itemsize, src)
         _ops.delta_encode(src.data, dst, n, self.dtype, self.astype)
         return finish(dst, self.astype, (n,), "C", src.host)

@@ -17,7 +17,7 @@ run() {  # name limit cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout=900 -p no:cacheprovider -rf ;;
+    tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchprof) run rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o bench -- python3 bench.py ;;
