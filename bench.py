@@ -101,12 +101,8 @@ def pmc_traffic():
     return int(sum(vals) / len(vals)), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(seconds: float = 10.0):
-    """Reference Shuffle(4) enc+dec on one core, time-bounded sample."""
-    x = np.random.default_rng(0).integers(0, 256, CHUNK, dtype=np.uint8)
-    enc = np.empty_like(x)
-    dec = np.empty_like(x)
-    kind = "port"
+def _ref_shuffle_fns():
+    """(encode, decode, kind, description) of the CPU Shuffle baseline."""
     try:
         from oracle import refload
 
@@ -131,6 +127,48 @@ def cpu_baseline(seconds: float = 10.0):
             nporacle.unshuffle_into(a, b, es)
 
         src_desc = "oracle/ncoracle.c restatement of _shuffle.pyx:11-30 (-O3, no -march)"
+        kind = "port"
+    return do_enc, do_dec, kind, src_desc
+
+
+def _cpu_worker(args):
+    """One process of the parallel leg: its own 64 MiB chunk, enc+dec until
+    the shared deadline; returns (bytes, seconds)."""
+    seed, deadline = args
+    do_enc, do_dec, _, _ = _ref_shuffle_fns()
+    x = np.random.default_rng(seed).integers(0, 256, 64 * MiB, dtype=np.uint8)
+    enc, dec = np.empty_like(x), np.empty_like(x)
+    do_enc(x, enc, 4)
+    t0 = time.perf_counter()
+    n = 0
+    while time.time() < deadline or n == 0:
+        do_enc(x, enc, 4)
+        do_dec(enc, dec, 4)
+        n += 1
+    return 2 * x.nbytes * n, time.perf_counter() - t0
+
+
+def cpu_baseline_parallel(procs: int, seconds: float = 5.0):
+    """The reference loop in `procs` processes at once (the reference holds the
+    GIL, so a Zarr reader scales over processes, not threads).  Forked BEFORE
+    the GPU is initialised (never fork or exec after HIP init)."""
+    import multiprocessing as mp
+
+    deadline = time.time() + 1.0 + seconds
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(100 + i, deadline) for i in range(procs)])
+    total = sum(b for b, _ in res)
+    el = max(t for _, t in res)
+    return {"value": round(total / GiB / el, 3), "unit": "GiB/s", "cores": procs,
+            "sample": f"{procs} processes x Shuffle(4) encode+decode of their own 64 MiB chunk for {el:.1f} s"}
+
+
+def cpu_baseline(seconds: float = 10.0):
+    """Reference Shuffle(4) enc+dec on one core, time-bounded sample."""
+    x = np.random.default_rng(0).integers(0, 256, CHUNK, dtype=np.uint8)
+    enc = np.empty_like(x)
+    dec = np.empty_like(x)
+    do_enc, do_dec, kind, src_desc = _ref_shuffle_fns()
     do_enc(x, enc, 4)  # warm
     do_dec(enc, dec, 4)
     assert np.array_equal(dec, x)
@@ -373,11 +411,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="processes of the parallel CPU leg (the GPU box's CPU share is 16)")
     ap.add_argument("--extra", action="store_true", help="also time C2(f64)/C3/C4/C5 on rank 0")
     ap.add_argument("--e2e", action="store_true", help="also time the host->host pipelined path")
     ap.add_argument("--next", action="store_true",
                     help="also time the SURVEY §8f next rows (checksum32 family, PackBits, AsType)")
     args = ap.parse_args()
+
+    # the multi-process CPU leg forks, so it runs before anything touches the GPU
+    cpu_par = None
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu and args.cpu_procs > 1:
+        cpu_par = cpu_baseline_parallel(args.cpu_procs)
 
     dist, rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", local)
@@ -434,6 +479,8 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            if cpu_par is not None:
+                result["cpu_baseline"]["parallel"] = cpu_par
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
