@@ -58,7 +58,7 @@ register_codec(PackBits)
 
 from . import batch  # noqa: E402,F401
 from . import blosc_shuffle  # noqa: E402,F401  (Blosc's per-block shuffle filters)
-from . import chunks  # noqa: E402,F401  (Zarr-style batched / host-streamed chunk pipelines)  (batched chunk API and fused pipelines)
+from . import chunks  # noqa: E402,F401  (Zarr-style batched / host-streamed chunk pipelines)
 
 __version__ = "0.1.0"
 
