@@ -235,6 +235,48 @@ def run_step_timing(args, dev, dist, rank, world):
     return elapsed, gpu_ms / (2 * args.steps)
 
 
+def run_c5_timing(args, dev, dist, rank, world):
+    """configs[4]: 8192 x 1 MiB fp32 chunks, Shuffle(4) + Fletcher32 fused,
+    sharded over ranks by contiguous chunk ranges (shard.chunk_range, no
+    collective); one step = encode + verified decode of the rank's chunks.
+    Returns (elapsed_s, mean launch ms, local chunks)."""
+    from numcodecs_amd import batch, shard
+
+    lo, hi = shard.chunk_range(args.c5_chunks, rank, world)
+    b = hi - lo
+    g = torch.Generator(device=dev).manual_seed(1000 + lo)
+    x = torch.randn((b, MiB // 4), generator=g, device=dev, dtype=torch.float32)
+    enc = batch.shuffle_fletcher32_encode_chunks(x, 4)
+    dec = torch.empty((b, MiB), dtype=torch.uint8, device=dev)
+    _, status = batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=True)
+    assert torch.equal(dec.view(torch.float32), x), "C5 round trip failed"
+
+    def step():
+        batch.shuffle_fletcher32_encode_chunks(x, 4, out=enc)
+        batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # the decode's checksum verdicts of the last step: every chunk must match
+    _, status = batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=True)
+    assert torch.equal(dec.view(torch.float32), x), "C5 round trip failed after timing"
+    return elapsed, ev0.elapsed_time(ev1) / (2 * args.steps), b
+
+
 def extra_workloads(dev):
     """The other configurations of BASELINE.json, single GPU (reported under
     "extra", not the headline value)."""
@@ -413,11 +455,17 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="processes of the parallel CPU leg (the GPU box's CPU share is 16)")
+    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
+                    help="c2 (default, the metric's config): Shuffle(4) on one 256 MiB chunk per GPU; "
+                         "c5: 8192 x 1 MiB chunks + Fletcher32 sharded over the GPUs")
+    ap.add_argument("--c5-chunks", type=int, default=8192)
     ap.add_argument("--extra", action="store_true", help="also time C2(f64)/C3/C4/C5 on rank 0")
     ap.add_argument("--e2e", action="store_true", help="also time the host->host pipelined path")
     ap.add_argument("--next", action="store_true",
                     help="also time the SURVEY §8f next rows (checksum32 family, PackBits, AsType)")
     args = ap.parse_args()
+    if args.workload == "c5":
+        args.no_cpu = True  # the CPU baseline is defined for the metric's workload (c2)
 
     # the multi-process CPU leg forks, so it runs before anything touches the GPU
     cpu_par = None
@@ -428,10 +476,17 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    elapsed, launch_ms = run_step_timing(args, dev, dist, rank, world)
+    c5 = args.workload == "c5"
+    if c5:
+        elapsed, launch_ms, local = run_c5_timing(args, dev, dist, rank, world)
+    else:
+        elapsed, launch_ms = run_step_timing(args, dev, dist, rank, world)
     t = max_over_ranks(dist, elapsed)
     launch_ms = max_over_ranks(dist, launch_ms)
-    total_bytes = world * args.steps * 2 * CHUNK  # bytes into encode + decode, all ranks
+    if c5:  # strong scaling: the 8192 chunks are split over the ranks
+        total_bytes = args.steps * 2 * args.c5_chunks * MiB
+    else:  # weak scaling: one 256 MiB chunk per rank per step
+        total_bytes = world * args.steps * 2 * CHUNK  # bytes into encode + decode, all ranks
     value = total_bytes / GiB / t
 
     result = None
@@ -470,6 +525,22 @@ def main():
                 "timing": "HIP events bracketing the timed region on the launch stream / (2 x steps)",
             },
         }
+    if rank == 0 and c5:
+        per_launch = (local * (MiB + 4) + local * MiB)  # rank 0's chunks: payload in + encoded out
+        result["scaling"] = "strong"
+        result["data"] = "synthetic (torch.randn fp32 on device, 1 MiB chunks)"
+        result["config"] = {
+            "workload": f"configs[4]: {args.c5_chunks} x 1 MiB fp32 chunks, Shuffle(4) + Fletcher32 fused encode + "
+                        "verified decode, sharded by contiguous chunk ranges",
+            "chunks": args.c5_chunks, "chunk_bytes": MiB, "elementsize": 4,
+            "parallelism": f"chunk-sharded x{world} (no collective)",
+        }
+        result["roofline"].update({
+            "kernel": "k_shuffle_f32_enc / k_f32_unshuffle (fused Shuffle(4)+Fletcher32, 2N+4 bytes per chunk)",
+            "achieved": round(per_launch / (launch_ms * 1e-3) / 1e9, 1),
+            "frac": round(per_launch / (launch_ms * 1e-3) / 1e9 / PEAK_GBPS, 4),
+            "traffic": None, "traffic_source": None,
+        })
     if rank == 0 and args.extra:
         result["extra"] = extra_workloads(dev)
     if rank == 0 and args.e2e:
