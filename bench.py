@@ -514,7 +514,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_shuffle_enc<4> / k_shuffle_dec<4> (Shuffle(4) encode / decode; 2 x 256 MiB algorithmic bytes per launch each)",
+                "kernel": "k_shuffle_enc<4> / k_shuffle4_dec_pair (Shuffle(4) encode / decode; 2 x 256 MiB algorithmic bytes per launch each)",
                 "achieved": round(achieved, 1),
                 "peak": PEAK_GBPS,
                 "unit": "GB/s",

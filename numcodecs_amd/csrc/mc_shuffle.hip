@@ -248,6 +248,84 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
 }
 
 // ---------------------------------------------------------------------------
+// es = 4 with lane pairs on the plane side: lanes 2j and 2j+1 hold the quads
+// of 8 consecutive elements; one DPP pair swap (quad_perm [1,0,3,2], no LDS)
+// of two plane dwords lets the even lane own planes 0-1 and the odd lane
+// planes 2-3 of all 8 elements, so each plane access is 8 B per lane (one
+// store/load instruction writes/reads two 256-B runs) and a quad needs 2
+// plane instructions instead of 4.  Element side unchanged (16 B per lane,
+// lane-contiguous).
+// ---------------------------------------------------------------------------
+MC_DEV uint32_t mc_pair_swap(uint32_t v) {  // value of the partner lane (lane ^ 1)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
+template <bool BITROUND, bool NT, int QMUL>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_enc_pair(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
+    McBitRound br) {
+  using G = Geom<4, QMUL>;
+  const int tid = threadIdx.x;
+  const bool odd = tid & 1;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TE + (odd ? 2 * m.count : 0);
+    uint32_t w[G::Q][4];
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) load_quad<4, NT>(s + (size_t)(q * MC_BLOCK + tid) * 16, w[q]);
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      if constexpr (BITROUND) mc_bitround_quad<4>(w[q], br);
+      uint32_t p[4];
+      mc_quad_to_planes<4>(w[q], p);
+      // even keeps planes 0,1 and receives the odd lane's; odd keeps 2,3
+      const uint32_t r0 = mc_pair_swap(odd ? p[0] : p[2]);
+      const uint32_t r1 = mc_pair_swap(odd ? p[1] : p[3]);
+      const mc_u32x2 a = odd ? mc_u32x2{r0, p[2]} : mc_u32x2{p[0], r0};
+      const mc_u32x2 b = odd ? mc_u32x2{r1, p[3]} : mc_u32x2{p[1], r1};
+      uint8_t *pd = d + (size_t)(q * MC_BLOCK + (tid & ~1)) * 4;  // 8-B aligned pair base
+      mc_st8<NT>(pd, a);
+      mc_st8<NT>(pd + m.count, b);
+    }
+  }
+}
+
+template <bool NT, int QMUL>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_dec_pair(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles) {
+  using G = Geom<4, QMUL>;
+  const int tid = threadIdx.x;
+  const bool odd = tid & 1;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TE + (odd ? 2 * m.count : 0);
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TB;
+    mc_u32x2 a[G::Q], b[G::Q];
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      const uint8_t *ps = s + (size_t)(q * MC_BLOCK + (tid & ~1)) * 4;
+      a[q] = mc_ld8<NT>(ps);
+      b[q] = mc_ld8<NT>(ps + m.count);
+    }
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      // even holds planes 0,1 of both quads (.x = its own quad, .y = odd's);
+      // odd holds planes 2,3
+      const uint32_t r0 = mc_pair_swap(odd ? a[q].x : a[q].y);
+      const uint32_t r1 = mc_pair_swap(odd ? b[q].x : b[q].y);
+      uint32_t p[4], w[4];
+      if (odd) { p[0] = r0; p[1] = r1; p[2] = a[q].y; p[3] = b[q].y; }
+      else { p[0] = a[q].x; p[1] = b[q].x; p[2] = r0; p[3] = r1; }
+      mc_planes_to_quad<4>(p, w);
+      store_quad<4, NT>(d + (size_t)(q * MC_BLOCK + tid) * 16, w);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // software-pipelined persistent variants (register layout): the next tile's
 // loads are issued before this tile's stores, so waiting for them does not
 // wait for the stores (vmcnt retires loads and stores in issue order).
@@ -419,7 +497,9 @@ static int default_variant(size_t es, bool enc, size_t total_bytes, unsigned *gr
   if (total_bytes < ((size_t)64 << 20)) return V_REG;
   switch (es) {
     case 2: return V_REG | V_BIG4;                       // 6.34 / 6.22 TB/s
-    case 4: return enc ? (V_REG | V_BIG4) : (V_REG | V_BIG);  // 6.1 / 6.2 TB/s
+    // decode: lane pairs, 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
+    // profiles/r01/shuffle4_pair_ab.log); encode: the pair stores are slower
+    case 4: return enc ? (V_REG | V_BIG4) : (V_PAIR | V_BIG);
     case 8:  // lane pairs keep the 8-B element side lane-contiguous
       return enc ? V_PAIR : (V_PAIR | V_BIG);            // 5.89 / 6.11 TB/s
     default:
@@ -433,6 +513,14 @@ template <int ES, bool BR, bool NT>
 static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                           size_t ntiles, unsigned grid, const McBitRound &br, hipStream_t st) {
   using G = Geom<ES>;
+  if constexpr (ES == 4) {
+    if ((layout & 7) == V_PAIR) {
+      if (layout & V_BIG4) k_shuffle4_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG) k_shuffle4_enc_pair<BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else k_shuffle4_enc_pair<BR, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      return;
+    }
+  }
   if constexpr (ES == 8) {
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
@@ -465,7 +553,7 @@ static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
                             hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
   if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
-  if ((layout & 7) == V_PAIR && ES != 8) return MC_EINVAL;
+  if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
   else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
   return mc_last_launch();
@@ -475,6 +563,14 @@ template <int ES, bool NT>
 static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                           size_t ntiles, unsigned grid, hipStream_t st) {
   using G = Geom<ES>;
+  if constexpr (ES == 4) {
+    if ((layout & 7) == V_PAIR) {
+      if (layout & V_BIG4) k_shuffle4_dec_pair<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else if (layout & V_BIG) k_shuffle4_dec_pair<NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else k_shuffle4_dec_pair<NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      return;
+    }
+  }
   if constexpr (ES == 8) {
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG4) k_shuffle8_dec_pair<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
@@ -506,13 +602,15 @@ static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
                             size_t ntiles, unsigned grid, hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
   if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
-  if ((layout & 7) == V_PAIR && ES != 8) return MC_EINVAL;
+  if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
   if (variant & V_NO_NT) launch_dec_nt<ES, false>(layout, s, d, m, ntiles, grid, st);
   else launch_dec_nt<ES, true>(layout, s, d, m, ntiles, grid, st);
   return mc_last_launch();
 }
 
 static size_t tile_elems(size_t es, int variant) {
+  if ((variant & 7) == V_PAIR && es == 4)  // Geom<4, QMUL> tiles
+    return (variant & V_BIG4) ? 16384 : (variant & V_BIG) ? 8192 : 4096;
   if ((variant & 7) == V_PAIR)  // 256 lanes x NV 16-B units of 8-B elements
     return (variant & V_BIG4) ? 8192 : (variant & V_BIG) ? 4096 : 2048;
   const size_t te = es >= 16 ? 2048 : 4096;
@@ -566,7 +664,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   McBitRound nobr{};
   const McBitRound &brr = br ? *br : nobr;
   if ((variant & 7) != V_GENERIC) {
-    if ((variant & 7) == V_PAIR && es != 8) variant = V_REG | (variant & V_NO_NT);
+    if ((variant & 7) == V_PAIR && es != 8 && es != 4) variant = V_REG | (variant & V_NO_NT);
     if ((variant & 7) != V_REG && (variant & 7) != V_PAIR) variant &= ~(V_BIG | V_BIG4 | V_PIPE);
     if ((variant & 7) == V_PAIR) variant &= ~V_PIPE;
     if (variant & V_PIPE) variant &= ~V_GROUP_MASK;

@@ -25,7 +25,7 @@ OUT = os.path.join(ROOT, "gpurun_out")
 
 KERNELS = {
     "shuffle_enc": "k_shuffle_enc<",
-    "shuffle_dec": "k_shuffle_dec<",
+    "shuffle_dec": ("k_shuffle_dec<", "k_shuffle4_dec_pair<"),
     "shuffle_f32_enc": "k_shuffle_f32_enc<",
     "f32_unshuffle": "k_f32_unshuffle<",
     "map": "k_map<",
@@ -36,6 +36,10 @@ KERNELS = {
     "f32_partial": "k_f32_partial<",
 }
 ALGO_BYTES = {"shuffle_enc": 2 * 256 * 2**20, "shuffle_dec": 2 * 256 * 2**20}
+
+
+def _match(pat, name: str) -> bool:
+    return any(p in name for p in ((pat,) if isinstance(pat, str) else pat))
 
 
 def short(name: str) -> str:
@@ -60,7 +64,7 @@ def main():
                             r["Percentage"], r["MinNs"], r["MaxNs"]])
         for key, pat in KERNELS.items():
             for r in rows:
-                if pat in r["Name"]:
+                if _match(pat, r["Name"]):
                     k = summary["kernels"].setdefault(key, {})
                     k["name"] = short(r["Name"])
                     k["calls"] = int(r["Calls"])
@@ -75,7 +79,7 @@ def main():
         rows = list(csv.DictReader(open(fn)))
         for key, pat in KERNELS.items():
             vals = [float(r["Counter_Value"]) for r in rows
-                    if pat in r["Kernel_Name"] and r["Counter_Name"] == counter]
+                    if _match(pat, r["Kernel_Name"]) and r["Counter_Name"] == counter]
             if vals:
                 k = summary["kernels"].setdefault(key, {})
                 k[counter + "_KiB_median"] = statistics.median(vals)
