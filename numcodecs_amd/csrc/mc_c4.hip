@@ -29,7 +29,22 @@ struct C4Params {
   size_t n;      // elements
   McNum off;     // encode: offset in D;   decode: offset in f64
   McNum sc;      // encode: scale in D;    decode: scale in f64
+  double rcp;    // decode: RN(1 / scale), computed on the host
+  bool fastdiv;  // decode: divide by scale as mul + 2 FMA (mc_div_by_const)
 };
+
+// Correctly rounded a / b for a constant b from rcp = RN(1/b) (Markstein):
+// y = RN(a*rcp) is within an ulp of a/b, r = a - y*b is exact in one FMA,
+// and RN(y + r*rcp) is RN(a/b).  Used only where the host has checked that
+// a/b and r stay in the normal range (|b| in [2^-500, 2^500], |a| < 2^64);
+// tests/test_gpu_c4.py compares it with IEEE division on every int16 for 15
+// scales.  When r == 0, y is already the exact quotient (and keeps the sign
+// of a zero).
+MC_DEV double mc_div_by_const(double a, double b, double rcp) {
+  const double y = a * rcp;
+  const double r = __builtin_fma(-y, b, a);
+  return r == 0.0 ? y : __builtin_fma(r, rcp, y);
+}
 
 template <int D, int A>
 MC_DEV int64_t fso_enc(uint64_t xbits, const C4Params &p) {
@@ -43,7 +58,8 @@ MC_DEV int64_t fso_enc(uint64_t xbits, const C4Params &p) {
 template <int D, int A>
 MC_DEV uint64_t fso_dec(int64_t a, const C4Params &p) {
   McNum v = mc_num_cast(mc_num_i(a), A, MC_F8);
-  v = mc_num_binop(v, p.sc, MC_OP_DIV, MC_F8);
+  if (p.fastdiv) v = mc_num_f(mc_div_by_const(v.f, p.sc.f, p.rcp));
+  else v = mc_num_binop(v, p.sc, MC_OP_DIV, MC_F8);
   v = mc_num_binop(v, p.off, MC_OP_ADD, MC_F8);
   return mc_num_to_bits(mc_num_cast(v, MC_F8, D), D);
 }
@@ -126,44 +142,88 @@ MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)
   }
 }
 
+// Reduce pass over PAIRS of 4096-element tiles (one workgroup, four 16-B
+// loads per thread in flight): pair_sums[i] = total of tiles 2i and 2i+1,
+// first[i] = total of tile 2i.  The scan then runs over half as many values
+// (k_scan_sums: 8K totals in one round instead of 16K in two), and the apply
+// pass takes tile t's prefix as scan[t/2] + (t odd ? first[t/2] : 0).
 template <int D, int A>
-__global__ __launch_bounds__(MC_BLOCK) void k_c4_reduce(const uint8_t *__restrict__ src,
-                                                       uint64_t *__restrict__ sums, C4Params p) {
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_reduce2(const uint8_t *__restrict__ src,
+                                                        uint64_t *__restrict__ pair_sums,
+                                                        uint64_t *__restrict__ first, C4Params p) {
   constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
-  __shared__ uint64_t lds[MC_BLOCK / 64];
-  const size_t e0 = (size_t)blockIdx.x * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
-  uint32_t acc = 0;
-  if (e0 < p.n) {
-    uint32_t v[C4_PER];
-    load16_deltas<A, ES>(src, p.n, e0, v);
+  __shared__ uint64_t lds[2][MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t e0 = (size_t)blockIdx.x * 2 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t acc[2] = {0, 0};
+  uint32_t v[2][C4_PER];
 #pragma unroll
-    for (int k = 0; k < C4_PER; ++k) acc += v[k];
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) load16_deltas<A, ES>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    acc[0] += __shfl_xor(acc[0], off, 64);
+    acc[1] += __shfl_xor(acc[1], off, 64);
   }
-  uint64_t tot;
-  mc_block_excl_scan<false>(acc, lds, &tot);
-  if (threadIdx.x == 0) sums[blockIdx.x] = (uint32_t)tot;
+  if (lane == 0) {
+    lds[0][wave] = acc[0];
+    lds[1][wave] = acc[1];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, b = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) {
+      a += (uint32_t)lds[0][w];
+      b += (uint32_t)lds[1][w];
+    }
+    first[blockIdx.x] = a;
+    pair_sums[blockIdx.x] = (uint32_t)(a + b);
+  }
 }
 
 // scan of 16 consecutive deltas + FSO decode, staged through LDS for
-// lane-contiguous 16-B stores; `pre` = exclusive prefix of the thread
+// lane-contiguous 16-B stores; `pre` = exclusive prefix of the thread.
+// The staging image is addressed in 16-B units with unit u stored at
+// u ^ ((u >> 3) & 7): a thread's own DS units (written with ds_write_b128,
+// 8-lane groups) and the lane-contiguous read-back (ds_read_b128, 16-lane
+// groups) are then both conflict-free.  Unswizzled, the 16 ds_write_b32 per
+// thread at a 64-B lane stride were 16-way bank conflicts.
+MC_DEV int c4_swz(int u) { return u ^ ((u >> 3) & 7); }
+
 template <int D, int A>
 MC_DEV void c4_finish(uint8_t *dst, size_t tile, const uint32_t (&incl)[C4_PER], uint32_t pre,
                       uint8_t *outb, const C4Params &p) {
   constexpr int DS = D == MC_F4 ? 4 : 8;
+  constexpr int UPT = C4_PER * DS / 16;  // 16-B units per thread
+  mc_u32x4 *img = reinterpret_cast<mc_u32x4 *>(outb);
+  uint32_t o[C4_PER * DS / 4];
 #pragma unroll
   for (int k = 0; k < C4_PER; ++k) {
-    const uint64_t o = fso_dec<D, A>(mc_wrap((int64_t)(uint32_t)(pre + incl[k]), A), p);
-    if constexpr (DS == 4) reinterpret_cast<uint32_t *>(outb)[threadIdx.x * C4_PER + k] = (uint32_t)o;
-    else reinterpret_cast<uint64_t *>(outb)[threadIdx.x * C4_PER + k] = o;
+    const uint64_t x = fso_dec<D, A>(mc_wrap((int64_t)(uint32_t)(pre + incl[k]), A), p);
+    if constexpr (DS == 4) {
+      o[k] = (uint32_t)x;
+    } else {
+      o[2 * k] = (uint32_t)x;
+      o[2 * k + 1] = (uint32_t)(x >> 32);
+    }
   }
+#pragma unroll
+  for (int j = 0; j < UPT; ++j)
+    img[c4_swz((int)threadIdx.x * UPT + j)] = mc_u32x4{o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]};
   __syncthreads();
   const size_t tile_b0 = tile * (size_t)MC_SCAN_TILE * DS;
   const size_t nbytes = p.n * DS;
 #pragma unroll
   for (int r = 0; r < MC_SCAN_TILE * DS / 16 / MC_BLOCK; ++r) {
-    const size_t off = ((size_t)r * MC_BLOCK + threadIdx.x) * 16;
-    if (tile_b0 + off < nbytes)
-      mc_st16<true>(dst + tile_b0 + off, reinterpret_cast<const mc_u32x4 *>(outb)[r * MC_BLOCK + threadIdx.x]);
+    const int u = r * MC_BLOCK + (int)threadIdx.x;
+    const size_t off = (size_t)u * 16;
+    if (tile_b0 + off < nbytes) mc_st16<true>(dst + tile_b0 + off, img[c4_swz(u)]);
   }
 }
 
@@ -189,7 +249,8 @@ MC_DEV void c4_local_scan(const uint8_t *src, size_t tile, const C4Params &p, ui
 template <int D, int A>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict__ src,
                                                       uint8_t *__restrict__ dst,
-                                                      const uint64_t *__restrict__ sums,
+                                                      const uint64_t *__restrict__ pair_pre,
+                                                      const uint64_t *__restrict__ first,
                                                       C4Params p) {
   constexpr int DS = D == MC_F4 ? 4 : 8;
   __shared__ uint64_t red[MC_BLOCK / 64];
@@ -199,7 +260,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict
   c4_local_scan<D, A>(src, tile, p, v, run);
   uint64_t agg;
   const uint32_t excl = (uint32_t)mc_block_excl_scan<false>(run, red, &agg);
-  c4_finish<D, A>(dst, tile, v, (uint32_t)sums[tile] + excl, outb, p);
+  const uint32_t tile_pre = (uint32_t)pair_pre[tile >> 1] + ((tile & 1) ? (uint32_t)first[tile >> 1] : 0u);
+  c4_finish<D, A>(dst, tile, v, tile_pre + excl, outb, p);
 }
 
 // Single-pass decode with decoupled look-back (mc_scan.h): tiles numbered in
@@ -282,9 +344,11 @@ template <int D, int A>
 static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Params &p,
                       hipStream_t st) {
   const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  k_c4_reduce<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, sums, p);
-  mc_launch_scan_sums<false>(sums, ntiles, st);
-  k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, sums, p);
+  const size_t npairs = (ntiles + 1) / 2;  // workspace: 16 + 8 * ntiles >= 16 * npairs
+  uint64_t *pair = sums, *first = sums + npairs;
+  k_c4_reduce2<D, A><<<(unsigned)npairs, MC_BLOCK, 0, st>>>(s, pair, first, p);
+  mc_launch_scan_sums<false>(pair, npairs, st);
+  k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, pair, first, p);
 }
 
 // MCODEC_C4_VARIANT: 2 = single-pass look-back decode with an atomic tile
@@ -329,6 +393,18 @@ static bool c4_ok(const void *src, const void *dst, size_t n, int dtype, int ast
     }                                                                        \
   } while (0)
 
+// integer numerators (|a| < 2^64) divided by a scale in [2^-500, 2^500]: the
+// quotient and the FMA residual stay normal, so mc_div_by_const is exact.
+// MCODEC_FASTDIV=0 forces IEEE division (A/B and tests).
+static bool mc_fastdiv_ok(double scale) {
+  static const bool enabled = [] {
+    const char *e = getenv("MCODEC_FASTDIV");
+    return !(e && atoi(e) == 0);
+  }();
+  const double m = scale < 0 ? -scale : scale;
+  return enabled && m >= 0x1p-500 && m <= 0x1p500;
+}
+
 }  // namespace
 
 extern "C" {
@@ -341,6 +417,8 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
   p.n = n;
   p.off = mc_num_f(offset);
   p.sc = mc_num_f(scale);
+  p.rcp = 0.0;
+  p.fastdiv = false;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   hipStream_t st = (hipStream_t)stream;
@@ -364,6 +442,8 @@ int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n, in
   p.n = n;
   p.off = mc_num_f(offset);
   p.sc = mc_num_f(scale);
+  p.rcp = 1.0 / scale;
+  p.fastdiv = mc_fastdiv_ok(scale);
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   hipStream_t st = (hipStream_t)stream;

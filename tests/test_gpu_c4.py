@@ -104,3 +104,39 @@ def test_decode_schedules_identical(device, variant, dt, at):
             raw.data_ptr(), out.data_ptr(), n, _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype),
             sc3, off4, ws.data_ptr(), ws.numel(), variant, _ops.stream(raw)), "decode_variant")
         assert torch.equal(out, ref.view(torch.uint8).reshape(-1)), variant
+
+
+SCALES = [1e3, 0.1, 3.0, 7.5, 1.0 / 3.0, 1e-7, 12345.678, -2.5, 10.0, 1e300, 3e-300, 2.0**-500, 2.0**500,
+          0.9999999999999999, 1.0000000000000002]
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("scale", SCALES)
+def test_fused_decode_every_int16(device, dt, scale):
+    """The fused decode divides by the constant scale with one multiply and
+    two FMAs (mc_div_by_const) where the host allows it: every int16 value,
+    decoded, must equal numpy's (enc / scale) + offset cast to dt
+    (fixedscaleoffset.py:99-113)."""
+    a = np.arange(-32768, 32768, dtype="<i2")
+    rng = np.random.default_rng(7)
+    a = np.concatenate([a, rng.permutation(a)])  # every value, in two orders
+    offset = 1000.25
+    codecs = _chain(dt, "<i2", offset, scale)
+    enc = oracle.shuffle(oracle.delta_encode(a, "<i2"), 2)
+    dec = batch.FilterPipeline(codecs).decode(torch.from_numpy(enc).to(device)).cpu().numpy()
+    with np.errstate(all="ignore"):
+        ref = oracle.fso_decode(a, offset, scale, dt, "<i2")
+    assert dec.view(np.uint8).tobytes() == np.ascontiguousarray(ref).view(np.uint8).tobytes(), scale
+
+
+@pytest.mark.parametrize("at,scale", [("<i4", 1e6), ("<i4", 3.7), ("<u4", 0.013), ("<u2", 1e3)])
+def test_fused_decode_random_wide(device, at, scale):
+    rng = np.random.default_rng(11)
+    info = np.iinfo(at)
+    a = rng.integers(info.min, info.max, 1 << 20, endpoint=True).astype(at)
+    codecs = _chain("<f8", at, -3.5, scale)
+    enc = oracle.shuffle(oracle.delta_encode(a, at), np.dtype(at).itemsize)
+    dec = batch.FilterPipeline(codecs).decode(torch.from_numpy(enc).to(device)).cpu().numpy()
+    with np.errstate(all="ignore"):
+        ref = oracle.fso_decode(a, -3.5, scale, "<f8", at)
+    assert dec.view(np.uint8).tobytes() == np.ascontiguousarray(ref).view(np.uint8).tobytes()
