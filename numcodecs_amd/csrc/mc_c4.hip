@@ -89,27 +89,37 @@ MC_DEV void unpack_quad(const uint32_t (&w)[ES], int64_t (&d)[4]) {
   }
 }
 
-template <int D, int A>
+template <int D, int A, int STEPS = MC_SCAN_STEPS>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__ src,
                                                     uint8_t *__restrict__ dst, C4Params p) {
   constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
   constexpr int DS = D == MC_F4 ? 4 : 8;
-  const size_t tile_e0 = (size_t)blockIdx.x * MC_SCAN_TILE;
+  const size_t tile_e0 = (size_t)blockIdx.x * (4 * STEPS * MC_BLOCK);
+  const int lane = threadIdx.x & 63;
+  // all steps' loads first (n % 16 == 0: quads are whole)
+  uint64_t x[STEPS][4];
 #pragma unroll
-  for (int q = 0; q < MC_SCAN_STEPS; ++q) {
+  for (int q = 0; q < STEPS; ++q) {
     const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
-    if (e >= p.n) continue;  // n % 16 == 0: quads are whole
-    uint64_t x[4];
-    mc_load4(src + e * DS, DS, x);
+    if (e < p.n) {
+      mc_load4(src + e * DS, DS, x[q]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[q][k] = 0;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < STEPS; ++q) {
+    const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
     int64_t a[4], d[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = fso_enc<D, A>(x[k], p);
-    if (e > 0) {
-      const int64_t prev = fso_enc<D, A>(mc_load_elem(src, e - 1, DS), p);
-      d[0] = mc_wrap(a[0] - prev, A);
-    } else {
-      d[0] = a[0];
-    }
+    for (int k = 0; k < 4; ++k) a[k] = fso_enc<D, A>(x[q][k], p);
+    // the element before the quad is the last one of lane - 1's quad; lane 0
+    // reads it (A is at most 32 bits wide, so differences mod 2^32 suffice)
+    int64_t prev = (int64_t)(int32_t)__shfl_up((uint32_t)a[3], 1, 64);
+    if (lane == 0 && e > 0 && e < p.n) prev = fso_enc<D, A>(mc_load_elem(src, e - 1, DS), p);
+    if (e >= p.n) continue;
+    d[0] = e > 0 ? mc_wrap(a[0] - prev, A) : a[0];
 #pragma unroll
     for (int k = 1; k < 4; ++k) d[k] = mc_wrap(a[k] - a[k - 1], A);
     uint32_t w[ES], pl[ES];
@@ -336,6 +346,8 @@ static void c4_decode_lb(const uint8_t *s, uint8_t *d, uint8_t *ws, const C4Para
 
 template <int D, int A>
 static void c4_encode(const uint8_t *s, uint8_t *d, const C4Params &p, hipStream_t st) {
+  // 4 quads per thread: 8 and 16 measured slower (77.6 / 93.0 vs 70.6 us for
+  // n = 64 Mi, register pressure)
   const unsigned grid = (unsigned)((p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE);
   k_c4_enc<D, A><<<grid, MC_BLOCK, 0, st>>>(s, d, p);
 }
