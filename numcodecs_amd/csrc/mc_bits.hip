@@ -150,29 +150,35 @@ __global__ __launch_bounds__(MC_BLOCK) void k_unpackbits(const uint8_t *__restri
 // 1 KiB contiguously (lane l writes bools [o, o + 16) with o = base + 1024v +
 // 16l); the 2 packed bytes behind them (encoded offsets 1 + o/8 and 2 + o/8)
 // come from one 8-byte load at the dword boundary below and v_alignbyte.
+template <int V>
 __global__ __launch_bounds__(MC_BLOCK) void k_unpackbits_wide(const uint8_t *__restrict__ src,
                                                               size_t src_bytes,
                                                               uint8_t *__restrict__ dst, size_t n) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t base = ((size_t)blockIdx.x * (MC_BLOCK / 64) + wave) * 4096;
+  const size_t base = ((size_t)blockIdx.x * (MC_BLOCK / 64) + wave) * (1024 * V);
+  uint32_t x[V];
 #pragma unroll
-  for (int v = 0; v < 4; ++v) {
+  for (int v = 0; v < V; ++v) {  // every load first
     const size_t o = base + 1024 * (size_t)v + 16 * (size_t)lane;
-    if (o >= n) break;
     const size_t e = 1 + o / 8;  // encoded offset of the first packed byte
     const size_t a = e & ~(size_t)3;
-    uint32_t x;
-    if (a + 8 <= src_bytes) {
+    if (o < n && a + 8 <= src_bytes) {
       mc_u32x2 w;  // dword aligned (a % 8 may be 4): dwordx2 at dword alignment
       __builtin_memcpy(&w, __builtin_assume_aligned(src + a, 4), 8);
-      x = __builtin_amdgcn_alignbyte(w.y, w.x, (uint32_t)(e - a));
+      x[v] = __builtin_amdgcn_alignbyte(w.y, w.x, (uint32_t)(e - a));
+    } else if (o < n) {
+      x[v] = (uint32_t)src[e] | (e + 1 < src_bytes ? (uint32_t)src[e + 1] << 8 : 0u);
     } else {
-      x = (uint32_t)src[e] | (e + 1 < src_bytes ? (uint32_t)src[e + 1] << 8 : 0u);
+      x[v] = 0;
     }
-    const uint64_t lo = unpack8(x & 0xffu), hi = unpack8((x >> 8) & 0xffu);
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const size_t o = base + 1024 * (size_t)v + 16 * (size_t)lane;
+    const uint64_t lo = unpack8(x[v] & 0xffu), hi = unpack8((x[v] >> 8) & 0xffu);
     if (o + 16 <= n) {
       mc_st16<true>(dst + o, mc_u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)});
-    } else {
+    } else if (o < n) {
       for (int i = 0; i < 16 && o + i < n; ++i) dst[o + i] = (uint8_t)((i < 8 ? lo : hi) >> (8 * (i & 7)));
     }
   }
@@ -205,10 +211,15 @@ int mc_unpackbits(const void *src, size_t src_bytes, void *dst, size_t n, mc_str
   if (src_bytes < 1 || !src || (n && !dst)) return MC_EINVAL;
   if (n > 8 * (src_bytes - 1)) return MC_EINVAL;
   if (n == 0) return MC_OK;
+  // 4 KiB of bools per wave: 2, 8 and 16 KiB measured slower (65.7-71.0,
+  // 71.2-71.9, 76.7-78.9 vs 66.6-66.8 us for 256 MiB); staging the packed
+  // bytes through LDS with 16-B loads was slower too (78 us)
+  constexpr int V = 4;
   if (((uintptr_t)src & 3) == 0 && ((uintptr_t)dst & 15) == 0) {
-    const size_t blocks = (n + 4 * 4096 - 1) / (4 * 4096);
+    const size_t per_block = (size_t)4 * 1024 * V;
+    const size_t blocks = (n + per_block - 1) / per_block;
     if (blocks > 0x7fffffffu) return MC_EINVAL;
-    k_unpackbits_wide<<<(unsigned)blocks, MC_BLOCK, 0, (hipStream_t)stream>>>(
+    k_unpackbits_wide<V><<<(unsigned)blocks, MC_BLOCK, 0, (hipStream_t)stream>>>(
         static_cast<const uint8_t *>(src), src_bytes, static_cast<uint8_t *>(dst), n);
     return mc_last_launch();
   }
