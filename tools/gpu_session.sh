@@ -22,7 +22,11 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     benchprof) run rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o bench -- python3 bench.py ;;
     benchx) run bench_extra 900 python bench.py --extra --no-cpu ;;
-    profx) run rocprof_extra 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_x -o bench -- python3 bench.py --extra --no-cpu --steps 10 ;;
+    profx) run rocprof_extra 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_extra -o bench -- python3 bench.py --extra --no-cpu --steps 10 ;;
+    pmcx) run pmc_fetch_x 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_fetch_extra -o bench -- python3 bench.py --extra --no-cpu --steps 5 --warmup 1
+          run pmc_write_x 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_write_extra -o bench -- python3 bench.py --extra --no-cpu --steps 5 --warmup 1 ;;
     e2e) run bench_e2e 900 python bench.py --e2e --no-cpu --steps 20 ;;
     multi) run bench_multi2 600 env MCODEC_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     probe) run probe_enc4 600 python tools/probe_enc.py 4 ;;

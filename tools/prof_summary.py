@@ -34,6 +34,12 @@ KERNELS = {
     "scan_reduce": "k_scan_reduce<",
     "scan_apply": "k_scan_apply<",
     "f32_partial": "k_f32_partial<",
+    "shuffle8_enc_pair": "k_shuffle8_enc_pair<",
+    "shuffle8_dec_pair": "k_shuffle8_dec_pair<",
+    "c4_enc": "k_c4_enc<",
+    "c4_reduce2": "k_c4_reduce2<",
+    "c4_apply": "k_c4_apply<",
+    "scan_sums": "k_scan_sums<",
 }
 ALGO_BYTES = {"shuffle_enc": 2 * 256 * 2**20, "shuffle_dec": 2 * 256 * 2**20}
 
@@ -50,13 +56,14 @@ def short(name: str) -> str:
 
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    tag = sys.argv[2] if len(sys.argv) > 2 else ""  # "" = headline, "_extra" = bench.py --extra
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
     summary = {"round": rnd, "kernels": {}}
-    stats_fn = os.path.join(OUT, "prof_kt", "bench_kernel_stats.csv")
+    stats_fn = os.path.join(OUT, "prof_kt" + tag, "bench_kernel_stats.csv")
     if os.path.exists(stats_fn):
         rows = list(csv.DictReader(open(stats_fn)))
-        with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as f:
+        with open(os.path.join(dst, f"kernel_stats{tag}.csv"), "w", newline="") as f:
             w = csv.writer(f)
             w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
             for r in rows:
@@ -73,7 +80,7 @@ def main():
                         k["algorithmic_bytes_per_launch"] = ALGO_BYTES[key]
                         k["achieved_GBps"] = round(ALGO_BYTES[key] / float(r["AverageNs"]), 1)
     for sub, counter in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
-        fn = os.path.join(OUT, sub, "bench_counter_collection.csv")
+        fn = os.path.join(OUT, sub + tag, "bench_counter_collection.csv")
         if not os.path.exists(fn):
             continue
         rows = list(csv.DictReader(open(fn)))
@@ -92,7 +99,7 @@ def main():
             if key in ALGO_BYTES:
                 k["traffic_over_algorithmic"] = round((fetch + write) / ALGO_BYTES[key], 4)
     summary["correction"] = "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024), MI355X_MICROARCH.md HBM section"
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+    with open(os.path.join(dst, f"pmc_summary{tag}.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1))
 
