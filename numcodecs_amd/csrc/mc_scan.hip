@@ -19,6 +19,10 @@
 //     a running carry (k_scan_rows), single pass.
 #include "mc_scan.h"
 
+#include <stdlib.h>
+
+#include <type_traits>
+
 namespace {
 
 // 4 consecutive elements i0..i0+3 of dtype a (as accumulation values in d)
@@ -394,14 +398,168 @@ static void launch_int_scan(const uint8_t *s, uint8_t *d, size_t n, int a, int d
   k_scan_apply<OR_OP, A_, D_, VEC><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, dt, sums);
 }
 
+// ---------------------------------------------------------------------------
+// Fast path for same-width integer Delta decode (astype == dtype, 16-B
+// aligned): a thread owns 32 consecutive bytes (DS_PER = 32/ES elements: two
+// 16-B vectors), so a tile of DS_PER * 256 elements (8 KiB) needs one block
+// scan, and the reduce pass covers groups of DS_GROUP tiles (32 KiB per
+// workgroup, all loads in flight at once) so that the tile-total scan runs
+// over groups only: tile t's prefix = group_pre[t / DS_GROUP] + part[t], with
+// part[t] the sum of the tiles before t in its group.  Arithmetic is modular
+// on the raw bits (mod 2^32 for ES <= 4, wrapped to the dtype width by the
+// store) -- exactly numpy's wrapping add.
+// ---------------------------------------------------------------------------
+constexpr int DS_GROUP = 4;
+
+template <int ES>
+using dacc_t = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
+
+template <int ES>
+constexpr int ds_per() { return 32 / ES; }
+template <int ES>
+constexpr size_t ds_tile() { return (size_t)ds_per<ES>() * MC_BLOCK; }
+
+// the values of elements [e0, e0 + PER) (zeros past n)
+template <int ES>
+MC_DEV void ds_load(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v)[ds_per<ES>()]) {
+  constexpr int PER = ds_per<ES>();
+  if (e0 + PER <= n) {
+    mc_u32x4 w[2];
+    w[0] = mc_ld16<true>(src + e0 * ES);
+    w[1] = mc_ld16<true>(src + e0 * ES + 16);
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(w);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if constexpr (ES == 1) v[i] = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      else if constexpr (ES == 2) v[i] = (d[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      else if constexpr (ES == 4) v[i] = d[i];
+      else v[i] = ((uint64_t)d[2 * i + 1] << 32) | d[2 * i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = e0 + i < n ? (dacc_t<ES>)mc_load_elem(src, e0 + i, ES) : 0;
+  }
+}
+
+template <int ES>
+MC_DEV void ds_store(uint8_t *dst, size_t n, size_t e0, const dacc_t<ES> (&v)[ds_per<ES>()]) {
+  constexpr int PER = ds_per<ES>();
+  if (e0 + PER <= n) {
+    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if constexpr (ES == 1) d[i >> 2] |= ((uint32_t)v[i] & 0xffu) << (8 * (i & 3));
+      else if constexpr (ES == 2) d[i >> 1] |= ((uint32_t)v[i] & 0xffffu) << (16 * (i & 1));
+      else if constexpr (ES == 4) d[i] = (uint32_t)v[i];
+      else { d[2 * i] = (uint32_t)v[i]; d[2 * i + 1] = (uint32_t)((uint64_t)v[i] >> 32); }
+    }
+    mc_st16<true>(dst + e0 * ES, mc_u32x4{d[0], d[1], d[2], d[3]});
+    mc_st16<true>(dst + e0 * ES + 16, mc_u32x4{d[4], d[5], d[6], d[7]});
+  } else {
+    for (int i = 0; i < PER && e0 + i < n; ++i) mc_store_elem(dst, e0 + i, ES, (uint64_t)v[i]);
+  }
+}
+
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce(const uint8_t *__restrict__ src, size_t n,
+                                                          uint64_t *__restrict__ group_sums,
+                                                          uint64_t *__restrict__ part) {
+  constexpr int PER = ds_per<ES>();
+  constexpr size_t TE = ds_tile<ES>();
+  __shared__ uint64_t lds[DS_GROUP][MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t t0 = (size_t)blockIdx.x * DS_GROUP;  // first tile of the group
+  dacc_t<ES> v[DS_GROUP][PER];
+#pragma unroll
+  for (int h = 0; h < DS_GROUP; ++h) ds_load<ES>(src, n, (t0 + h) * TE + (size_t)threadIdx.x * PER, v[h]);
+  uint64_t acc[DS_GROUP];
+#pragma unroll
+  for (int h = 0; h < DS_GROUP; ++h) {
+    acc[h] = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) acc[h] += v[h][i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) acc[h] += __shfl_xor(acc[h], off, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) lds[h][wave] = acc[h];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t run = 0;
+    for (int h = 0; h < DS_GROUP; ++h) {
+      uint64_t tot = 0;
+      for (int w = 0; w < MC_BLOCK / 64; ++w) tot += lds[h][w];
+      part[t0 + h] = run;  // part[] has DS_GROUP * ngroups entries
+      run += tot;
+    }
+    group_sums[blockIdx.x] = run;
+  }
+}
+
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply(const uint8_t *__restrict__ src,
+                                                         uint8_t *__restrict__ dst, size_t n,
+                                                         const uint64_t *__restrict__ group_pre,
+                                                         const uint64_t *__restrict__ part) {
+  constexpr int PER = ds_per<ES>();
+  __shared__ uint64_t lds[MC_BLOCK / 64];
+  const size_t tile = blockIdx.x;
+  const size_t e0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * PER;
+  dacc_t<ES> v[PER];
+  ds_load<ES>(src, n, e0, v);
+  dacc_t<ES> run = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    run += v[i];
+    v[i] = run;
+  }
+  uint64_t tot;
+  const uint64_t excl = mc_block_excl_scan<false>((uint64_t)run, lds, &tot);
+  const dacc_t<ES> pre = (dacc_t<ES>)(group_pre[tile / DS_GROUP] + part[tile] + excl);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] += pre;
+  ds_store<ES>(dst, n, e0, v);
+}
+
+// workspace entries of the fast path: part[] (whole groups of tiles) + group sums
+static size_t dscan_ws_entries(size_t n, int es) {
+  const size_t te = (size_t)(32 / es) * MC_BLOCK;
+  const size_t ngroups = ((n + te - 1) / te + DS_GROUP - 1) / DS_GROUP;
+  return ngroups * DS_GROUP + ngroups;
+}
+
+// MCODEC_DSCAN=0 selects the generic three-pass kernels (A/B)
+static bool dscan_enabled() {
+  static const bool b = [] {
+    const char *e = getenv("MCODEC_DSCAN");
+    return !(e && atoi(e) == 0);
+  }();
+  return b;
+}
+
+template <int ES>
+static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, hipStream_t st) {
+  const size_t ntiles = (n + ds_tile<ES>() - 1) / ds_tile<ES>();
+  const size_t ngroups = (ntiles + DS_GROUP - 1) / DS_GROUP;
+  uint64_t *group = ws, *part = ws + ngroups;
+  k_dscan_reduce<ES><<<(unsigned)ngroups, MC_BLOCK, 0, st>>>(s, n, group, part);
+  mc_launch_scan_sums<false>(group, ngroups, st);
+  k_dscan_apply<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, group, part);
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
-  (void)astype;
   if (mc_is_float(dtype)) return 0;
-  return ((n + MC_SCAN_TILE - 1) / MC_SCAN_TILE) * sizeof(uint64_t);
+  const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const size_t fast = astype == dtype && dtype != MC_B1 ? dscan_ws_entries(n, mc_itemsize(dtype)) : 0;
+  return (generic > fast ? generic : fast) * sizeof(uint64_t);
 }
 
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
@@ -417,8 +575,18 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
     return mc_last_launch();
   }
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  if (!workspace || workspace_bytes < ntiles * sizeof(uint64_t)) return MC_ENOSPC;
+  if (!workspace || workspace_bytes < mc_delta_decode_workspace(n, astype, dtype)) return MC_ENOSPC;
   uint64_t *sums = static_cast<uint64_t *>(workspace);
+  if (astype == dtype && dtype != MC_B1 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0 &&
+      dscan_enabled()) {
+    switch (mc_itemsize(dtype)) {
+      case 1: launch_dscan<1>(s, d, n, sums, st); break;
+      case 2: launch_dscan<2>(s, d, n, sums, st); break;
+      case 4: launch_dscan<4>(s, d, n, sums, st); break;
+      default: launch_dscan<8>(s, d, n, sums, st); break;
+    }
+    return mc_last_launch();
+  }
   const bool vec = ((uintptr_t)src % (4 * mc_itemsize(astype)) == 0) &&
                    ((uintptr_t)dst % (4 * mc_itemsize(dtype)) == 0);
   if (dtype == MC_B1) {
