@@ -317,8 +317,17 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
     const dim3 grid(blocks_for(n), (unsigned)min(YMAX, nchunks - c0));
     const uint8_t *sc = s + c0 * src_stride;
     uint8_t *dc = d + c0 * dst_stride;
-    if (vec && dtype == MC_I2 && astype == MC_I2)
-      k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
+    // same-width integers: wrapping differences have the same bits whatever
+    // the signedness, so every such pair runs the signed instantiation
+    const int same = (dtype == astype && dtype != MC_B1 && !mc_is_float(dtype)) ? ss : 0;
+    if (vec && same == 1)
+      k_delta_enc<MC_I1, MC_I1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I1, MC_I1, src_stride, dst_stride);
+    else if (vec && same == 2)
+      k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I2, MC_I2, src_stride, dst_stride);
+    else if (vec && same == 4)
+      k_delta_enc<MC_I4, MC_I4, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I4, MC_I4, src_stride, dst_stride);
+    else if (vec && same == 8)
+      k_delta_enc<MC_I8, MC_I8, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I8, MC_I8, src_stride, dst_stride);
     else if (vec)
       k_delta_enc<-1, -1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
     else

@@ -532,6 +532,42 @@ static size_t dscan_ws_entries(size_t n, int es) {
   return ngroups * DS_GROUP + ngroups;
 }
 
+// Batched same-width integer Delta decode: one workgroup per chunk walks it in
+// 8 KiB tiles (32 B per thread, one block scan per tile) with a running
+// carry; the next tile's loads are issued before the current tile's scan.
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_dscan_rows(const uint8_t *__restrict__ src,
+                                                        size_t src_stride,
+                                                        uint8_t *__restrict__ dst,
+                                                        size_t dst_stride, size_t n) {
+  constexpr int PER = ds_per<ES>();
+  constexpr size_t TE = ds_tile<ES>();
+  __shared__ uint64_t lds[MC_BLOCK / 64];
+  src += (size_t)blockIdx.x * src_stride;
+  dst += (size_t)blockIdx.x * dst_stride;
+  dacc_t<ES> carry = 0;
+  dacc_t<ES> nxt[PER];
+  ds_load<ES>(src, n, (size_t)threadIdx.x * PER, nxt);
+  for (size_t base = 0; base < n; base += TE) {
+    dacc_t<ES> v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = nxt[i];
+    if (base + TE < n) ds_load<ES>(src, n, base + TE + (size_t)threadIdx.x * PER, nxt);
+    dacc_t<ES> run = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      run += v[i];
+      v[i] = run;
+    }
+    uint64_t tot;
+    const dacc_t<ES> pre = carry + (dacc_t<ES>)mc_block_excl_scan<false>((uint64_t)run, lds, &tot);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] += pre;
+    ds_store<ES>(dst, n, base + (size_t)threadIdx.x * PER, v);
+    carry += (dacc_t<ES>)tot;
+  }
+}
+
 // MCODEC_DSCAN=0 selects the generic three-pass kernels (A/B)
 static bool dscan_enabled() {
   static const bool b = [] {
@@ -634,6 +670,18 @@ int mc_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst,
     const size_t as = mc_itemsize(astype), ds = mc_itemsize(dtype);
     const bool vec = ((uintptr_t)sc % (4 * as) == 0) && (src_stride % (4 * as) == 0) &&
                      ((uintptr_t)dc % (4 * ds) == 0) && (dst_stride % (4 * ds) == 0);
+    const bool al16 = ((uintptr_t)sc % 16 == 0) && (rows == 1 || src_stride % 16 == 0) &&
+                      ((uintptr_t)dc % 16 == 0) && (rows == 1 || dst_stride % 16 == 0);
+    if (astype == dtype && dtype != MC_B1 && al16 && dscan_enabled()) {
+      const unsigned g = (unsigned)rows;
+      switch (ds) {
+        case 1: k_dscan_rows<1><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n); break;
+        case 2: k_dscan_rows<2><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n); break;
+        case 4: k_dscan_rows<4><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n); break;
+        default: k_dscan_rows<8><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n); break;
+      }
+      continue;
+    }
     if (dtype == MC_B1) {
       if (vec) launch_rows<true, -1, -1, true>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
       else launch_rows<true, -1, -1, false>(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st);
