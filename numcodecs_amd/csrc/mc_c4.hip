@@ -33,19 +33,6 @@ struct C4Params {
   bool fastdiv;  // decode: divide by scale as mul + 2 FMA (mc_div_by_const)
 };
 
-// Correctly rounded a / b for a constant b from rcp = RN(1/b) (Markstein):
-// y = RN(a*rcp) is within an ulp of a/b, r = a - y*b is exact in one FMA,
-// and RN(y + r*rcp) is RN(a/b).  Used only where the host has checked that
-// a/b and r stay in the normal range (|b| in [2^-500, 2^500], |a| < 2^64);
-// tests/test_gpu_c4.py compares it with IEEE division on every int16 for 15
-// scales.  When r == 0, y is already the exact quotient (and keeps the sign
-// of a zero).
-MC_DEV double mc_div_by_const(double a, double b, double rcp) {
-  const double y = a * rcp;
-  const double r = __builtin_fma(-y, b, a);
-  return r == 0.0 ? y : __builtin_fma(r, rcp, y);
-}
-
 template <int D, int A>
 MC_DEV int64_t fso_enc(uint64_t xbits, const C4Params &p) {
   McNum v = mc_num_from_bits(xbits, D);
@@ -404,18 +391,6 @@ static bool c4_ok(const void *src, const void *dst, size_t n, int dtype, int ast
       }                                                                      \
     }                                                                        \
   } while (0)
-
-// integer numerators (|a| < 2^64) divided by a scale in [2^-500, 2^500]: the
-// quotient and the FMA residual stay normal, so mc_div_by_const is exact.
-// MCODEC_FASTDIV=0 forces IEEE division (A/B and tests).
-static bool mc_fastdiv_ok(double scale) {
-  static const bool enabled = [] {
-    const char *e = getenv("MCODEC_FASTDIV");
-    return !(e && atoi(e) == 0);
-  }();
-  const double m = scale < 0 ? -scale : scale;
-  return enabled && m >= 0x1p-500 && m <= 0x1p500;
-}
 
 }  // namespace
 

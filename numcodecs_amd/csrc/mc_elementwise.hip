@@ -26,10 +26,13 @@ enum MapKind { K_CAST = 0, K_FSO_ENC = 1, K_FSO_DEC = 2, K_QUANTIZE = 3 };
 struct MapParams {
   int d, t1, t2, a;  // input dtype, compute dtypes, output dtype
   McNum s0, s1;      // scalars in their compute dtypes
+  double rcp = 0.0;      // FSO decode: RN(1 / scale) (host)
+  bool fastdiv = false;  // FSO decode: integer input, f64 division by the constant scale
 };
 
 template <int KIND>
-MC_DEV McNum map_op(McNum x, int d, int t1, int t2, int a, const McNum &s0, const McNum &s1) {
+MC_DEV McNum map_op(McNum x, int d, int t1, int t2, int a, const McNum &s0, const McNum &s1,
+                    double rcp = 0.0, bool fastdiv = false) {
   if constexpr (KIND == K_CAST) {
     return mc_num_cast(x, d, a);
   } else if constexpr (KIND == K_FSO_ENC) {  // s0 = offset (t1), s1 = scale (t2)
@@ -41,7 +44,8 @@ MC_DEV McNum map_op(McNum x, int d, int t1, int t2, int a, const McNum &s0, cons
     return mc_num_cast(v, t2, a);
   } else if constexpr (KIND == K_FSO_DEC) {  // s0 = scale (t1), s1 = offset (t2)
     McNum v = mc_num_cast(x, d, t1);
-    v = mc_num_binop(v, s0, MC_OP_DIV, t1);
+    if (fastdiv) v = mc_num_f(mc_div_by_const(v.f, s0.f, rcp));  // t1 == f64, integer x
+    else v = mc_num_binop(v, s0, MC_OP_DIV, t1);
     v = mc_num_cast(v, t1, t2);
     v = mc_num_binop(v, s1, MC_OP_ADD, t2);
     return mc_num_cast(v, t2, a);
@@ -74,20 +78,20 @@ __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ sr
         mc_load4(src + i0 * ss, ss, e);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          o[k] = mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e[k], d), d, t1, t2, a, prm.s0, prm.s1), a);
+          o[k] = mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e[k], d), d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a);
         mc_store4(dst + i0 * ds, ds, o);
       } else {
         for (size_t i = i0; i < n; ++i)
           mc_store_elem(dst, i, ds,
                         mc_num_to_bits(map_op<KIND>(mc_num_from_bits(mc_load_elem(src, i, ss), d),
-                                                    d, t1, t2, a, prm.s0, prm.s1), a));
+                                                    d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a));
       }
     }
   } else {
     for (size_t i = base + threadIdx.x; i < n && i < base + ELEMS_PER_BLOCK; i += MC_BLOCK)
       mc_store_elem_u(dst, i, ds,
                       mc_num_to_bits(map_op<KIND>(mc_num_from_bits(mc_load_elem_u(src, i, ss), d),
-                                                  d, t1, t2, a, prm.s0, prm.s1), a));
+                                                  d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a));
   }
 }
 
@@ -285,6 +289,11 @@ int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3, int 
                   double scale, double offset, mc_stream_t stream) {
   if (!mc_is_float(t3) || !mc_is_float(t4)) return MC_EINVAL;
   MapParams p{astype, t3, t4, dtype, num_scalar(t3, scale, 0), num_scalar(t4, offset, 0)};
+  // integer inputs (exact in f64) divided in f64 by the constant scale
+  if (t3 == MC_F8 && !mc_is_float(astype) && astype != MC_B1) {
+    p.rcp = 1.0 / scale;
+    p.fastdiv = mc_fastdiv_ok(scale);
+  }
   return launch_map<K_FSO_DEC>(src, dst, n, p, (hipStream_t)stream);
 }
 

@@ -140,3 +140,16 @@ def test_fused_decode_random_wide(device, at, scale):
     with np.errstate(all="ignore"):
         ref = oracle.fso_decode(a, -3.5, scale, "<f8", at)
     assert dec.view(np.uint8).tobytes() == np.ascontiguousarray(ref).view(np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("scale", SCALES)
+def test_fso_decode_every_int16(device, dt, scale):
+    """The standalone FixedScaleOffset decode (csrc/mc_elementwise.hip) uses
+    the same constant division for integer inputs: every int16 value."""
+    a = np.arange(-32768, 32768, dtype="<i2")
+    codec = FixedScaleOffset(offset=-7.125, scale=scale, dtype=dt, astype="<i2")
+    dec = codec.decode(torch.from_numpy(a).to(device)).cpu().numpy()
+    with np.errstate(all="ignore"):
+        ref = oracle.fso_decode(a, -7.125, scale, dt, "<i2")
+    assert dec.view(np.uint8).tobytes() == np.ascontiguousarray(ref).view(np.uint8).tobytes(), scale
