@@ -59,6 +59,7 @@ register_codec(PackBits)
 from . import batch  # noqa: E402,F401
 from . import blosc_shuffle  # noqa: E402,F401  (Blosc's per-block shuffle filters)
 from . import chunks  # noqa: E402,F401  (Zarr-style batched / host-streamed chunk pipelines)
+from . import graphs  # noqa: E402,F401  (HIP-graph captured chunk pipelines)
 
 __version__ = "0.1.0"
 
@@ -80,6 +81,7 @@ __all__ = [
     "batch",
     "blosc_shuffle",
     "chunks",
+    "graphs",
     "codec_registry",
     "get_codec",
     "register_codec",

@@ -171,7 +171,7 @@ def test_library_host_queries_need_no_gpu():
     lib = _native.lib
     assert lib.mc_strerror(-22) == b"invalid argument"
     assert lib.mc_fletcher32_workspace(1 << 20) >= 12
-    assert lib.mc_delta_decode_workspace(1 << 20, 2, 2) == ((1 << 20) // 4096) * 8
+    assert lib.mc_delta_decode_workspace(1 << 20, 2, 2) >= ((1 << 20) // 4096) * 8  # tile totals (+ group offsets)
     assert lib.mc_delta_decode_workspace(100, 10, 10) == 0  # float: serial, none
 
 
