@@ -8,6 +8,8 @@ synchronises except where a result must be inspected on the host
 
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import torch
 
@@ -29,7 +31,14 @@ def dtype_code(dt) -> int:
         ) from None
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream(t: torch.Tensor) -> int:
+    """hipStream_t of torch's current stream on `t`'s device (the raw handle
+    straight from torch's C++ side: the Python wrapper costs ~4 us a call)."""
+    if _raw_stream is not None:
+        return _raw_stream(t.device.index)
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
@@ -37,7 +46,13 @@ def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
 
 
+_NO_GUARD = contextlib.nullcontext()
+
+
 def _guard(t: torch.Tensor):
+    """Make `t`'s device current for the call (a no-op when it already is)."""
+    if t.device.index == torch.cuda.current_device():
+        return _NO_GUARD
     return torch.cuda.device(t.device)
 
 

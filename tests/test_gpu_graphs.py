@@ -64,3 +64,16 @@ def test_graph_refuses_host_sync(device):
     x = torch.zeros((4, 1024), dtype=torch.int64, device=device)
     with pytest.raises(ValueError):
         GraphChain([Delta(dtype="<i8", astype="<i4")], x, "encode")
+
+
+def test_raw_stream_handle_matches_torch(device):
+    """_ops.stream reads the raw hipStream_t from torch's C++ side; it must be
+    the handle torch.cuda.current_stream reports, on the default and on a
+    side stream."""
+    from numcodecs_amd import _ops
+
+    x = torch.zeros(4, device=device)
+    assert _ops.stream(x) == torch.cuda.current_stream(device).cuda_stream
+    s = torch.cuda.Stream(device=device)
+    with torch.cuda.stream(s):
+        assert _ops.stream(x) == s.cuda_stream
