@@ -33,21 +33,13 @@ def _cast(buf, from_dt, to_dt):
 
 
 class AsType(Codec):
-    """Filter to convert data between different types.
+    """Cast chunks from `decode_dtype` to `encode_dtype` on encode and back on
+    decode (numcodecs id ``astype``), on the GPU.
 
-    Parameters
-    ----------
-    encode_dtype : dtype
-        Data type to use for encoded data.
-    decode_dtype : dtype, optional
-        Data type to use for decoded data.
-
-    Notes
-    -----
-    If `encode_dtype` is of lower precision than `decode_dtype`, please be
-    aware that data loss can occur by writing data to disk using this filter.
-    No checks are made to ensure the casting will work in that direction and
-    data corruption will occur.
+    The cast follows numpy's unsafe ``astype``: narrowing an integer wraps,
+    narrowing a float rounds to nearest-even, and float values outside the
+    integer range give the x86-64 results numpy produces.  A lossy
+    `encode_dtype` therefore loses data silently, exactly as in numcodecs.
     """
 
     codec_id = "astype"

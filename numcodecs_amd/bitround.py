@@ -32,16 +32,11 @@ max_bits = {
 
 
 class BitRound(Codec):
-    """Floating-point bit rounding codec
+    """Round float mantissas to `keepbits` bits (numcodecs id ``bitround``).
 
-    Drops a specified number of bits from the floating point mantissa,
-    leaving an array more amenable to compression (Klöwer et al. 2021).
-
-    Parameters
-    ----------
-    keepbits: int
-        The number of bits of the mantissa to keep.  Equal to the maximum for
-        the dtype means no transform.
+    Round-to-nearest-even on the integer view of each f2/f4/f8 value, so
+    the trailing mantissa bits become zero and compress well (Klöwer et al.
+    2021).  `keepbits` equal to the dtype's mantissa width is the identity.
     """
 
     codec_id = "bitround"

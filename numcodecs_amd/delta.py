@@ -31,28 +31,16 @@ def check_first_elements(firsts, dtype, astype) -> None:
 
 
 class Delta(Codec):
-    """Codec to encode data as the difference between adjacent values.
+    """Store each element as its difference from the previous one (the first
+    element as itself), numcodecs id ``delta``.
 
-    Parameters
-    ----------
-    dtype : dtype
-        Data type to use for decoded data.
-    astype : dtype, optional
-        Data type to use for encoded data.
+    `dtype` is the type differences are computed in (and decoded to);
+    `astype` (default: `dtype`) is the type they are stored as.  A narrow
+    integer `astype` wraps on overflow without any check, as in numcodecs.
+    Decoding is the running sum in `dtype` (numpy's ``cumsum`` order).
 
-    Notes
-    -----
-    If `astype` is an integer data type, please ensure that it is
-    sufficiently large to store encoded values. No checks are made and data
-    may become corrupted due to integer overflow if `astype` is too small.
-
-    Examples
-    --------
-    >>> import numpy as np
-    >>> import numcodecs_amd
-    >>> x = np.arange(100, 120, 2, dtype='i2')
-    >>> codec = numcodecs_amd.Delta(dtype='i2', astype='i1')
-    >>> codec.encode(x)  # doctest: +SKIP
+    >>> import numpy as np, numcodecs_amd
+    >>> numcodecs_amd.Delta(dtype='i2', astype='i1').encode(np.arange(100, 120, 2, dtype='i2'))  # doctest: +SKIP
     array([100,   2,   2,   2,   2,   2,   2,   2,   2,   2], dtype=int8)
     """
 

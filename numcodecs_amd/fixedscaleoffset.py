@@ -32,21 +32,12 @@ def _resolve(op, dtype, scalar):
 
 
 class FixedScaleOffset(Codec):
-    """Simplified version of the scale-offset filter available in HDF5.
-    Applies the transformation `(x - offset) * scale` to all chunks. Results
-    are rounded to the nearest integer but are not packed according to the
-    minimum number of bits.
+    """Fixed scale/offset encoding (numcodecs id ``fixedscaleoffset``), after
+    HDF5's scale-offset filter without the bit packing.
 
-    Parameters
-    ----------
-    offset : float
-        Value to subtract from data.
-    scale : float
-        Value to multiply by data.
-    dtype : dtype
-        Data type to use for decoded data.
-    astype : dtype, optional
-        Data type to use for encoded data.
+    encode: ``astype(round((x - offset) * scale))`` computed in `dtype` (numpy's
+    promotion of the Python scalars); decode: ``(y / scale) + offset`` in
+    float64, cast back to `dtype`.  `astype` defaults to `dtype`.
     """
 
     codec_id = "fixedscaleoffset"

@@ -16,12 +16,9 @@ __all__ = ["PackBits"]
 
 
 class PackBits(Codec):
-    """Codec to pack elements of a boolean array into bits in a uint8 array.
-
-    Notes
-    -----
-    The first element of the encoded array stores the number of bits that
-    were padded to complete the final byte.
+    """Booleans to bits, eight per byte, most significant bit first
+    (numcodecs id ``packbits``).  The encoded buffer starts with one byte
+    holding the number of padding bits in the last byte.
     """
 
     codec_id = "packbits"

@@ -27,16 +27,9 @@ def quantize_scale(digits) -> float:
 
 
 class Quantize(Codec):
-    """Lossy filter to reduce the precision of floating point data.
-
-    Parameters
-    ----------
-    digits : int
-        Desired precision (number of decimal digits).
-    dtype : dtype
-        Data type to use for decoded data.
-    astype : dtype, optional
-        Data type to use for encoded data.
+    """Keep about `digits` decimal digits of float data (numcodecs id
+    ``quantize``): values are rounded to a multiple of a power-of-two step
+    and stored as `astype` (default `dtype`).  Lossy; decode is a cast.
     """
 
     codec_id = "quantize"

@@ -22,12 +22,9 @@ __all__ = ["Shuffle"]
 
 
 class Shuffle(Codec):
-    """Codec providing shuffle
-
-    Parameters
-    ----------
-    elementsize : int
-        Size in bytes of the array elements.  Default = 4
+    """Byte shuffle (numcodecs id ``shuffle``): byte b of every
+    `elementsize`-byte element goes to plane b, planes stored one after
+    another.  `elementsize` <= 1 copies the bytes unchanged.
     """
 
     codec_id = "shuffle"
