@@ -166,7 +166,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
 
 enum FinalMode { F_SUM = 0, F_FOOTER = 1, F_VERIFY = 2 };
 
-// one thread per chunk: fold the chunk's slices, then
+// one workgroup per chunk: the 256 threads fold the chunk's slices (a large
+// chunk has thousands: a single thread walking them serially was the
+// bottleneck of a 256 MiB checksum), then
 //   F_SUM:    out[c] = checksum
 //   F_FOOTER: LE32 checksum at dst + c*dst_stride + nbytes (and out[c] if set)
 //   F_VERIFY: out[2c] = checksum, out[2c+1] = LE32 footer at src + c*src_stride + nbytes
@@ -174,17 +176,19 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
     const uint32_t *__restrict__ partials, unsigned nslices, size_t nchunks, int mode,
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t nbytes, uint32_t *__restrict__ out) {
-  const size_t c = (size_t)blockIdx.x * MC_BLOCK + threadIdx.x;
-  if (c >= nchunks) return;
-  uint64_t a = 0, b = 0;
-  uint32_t z = 0;
-  for (unsigned sl = 0; sl < nslices; ++sl) {
+  const size_t c = blockIdx.x;
+  F32Part p;
+  part_init(p);
+  for (unsigned sl = threadIdx.x; sl < nslices; sl += MC_BLOCK) {
     const uint32_t *q = partials + 3 * (c * nslices + sl);
-    a += q[0];
-    b += q[1];
-    z |= q[2];
+    p.s1 += q[0];
+    p.s2a += q[1];  // partial S2 already reduced: s2b stays 0
+    p.nz |= q[2];
   }
-  const uint32_t f = final_sum(mod_m(a), mod_m(b), z);
+  uint32_t a, b, z;
+  block_reduce(p, a, b, z);
+  if (threadIdx.x != 0) return;
+  const uint32_t f = final_sum(a, b, z);
   if (mode == F_SUM) {
     out[c] = f;
   } else if (mode == F_FOOTER) {
@@ -323,9 +327,8 @@ static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t d
   }
   int rc = mc_last_launch();
   if (rc != MC_OK) return rc;
-  const unsigned fgrid = (unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK);
-  k_f32_finalize<<<fgrid, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride, dst,
-                                             dst_stride, nbytes, out);
+  k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride,
+                                                         dst, dst_stride, nbytes, out);
   return mc_last_launch();
 }
 
@@ -432,7 +435,7 @@ int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void 
     else k_f32_partial<false, false><<<(unsigned)(nchunks * nsl), MC_BLOCK, 0, st>>>(d, dst_stride, nullptr, 0, chunk_bytes, nsl, partials);
     rc = mc_last_launch();
     if (rc != MC_OK) return rc;
-    k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+    k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(
         partials, nsl, nchunks, F_FOOTER, nullptr, 0, d, dst_stride, chunk_bytes, nullptr);
     return mc_last_launch();
   }
@@ -452,7 +455,7 @@ int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void 
   }
   int rc = mc_last_launch();
   if (rc != MC_OK) return rc;
-  k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+  k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(
       partials, (unsigned)m.tiles_per_chunk, nchunks, F_FOOTER, nullptr, 0, d, dst_stride,
       chunk_bytes, nullptr);
   return mc_last_launch();
@@ -496,7 +499,7 @@ int mc_fletcher32_unshuffle_batch(const void *src, size_t src_stride, void *dst,
   }
   int rc = mc_last_launch();
   if (rc != MC_OK) return rc;
-  k_f32_finalize<<<(unsigned)((nchunks + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(
+  k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(
       partials, (unsigned)m.tiles_per_chunk, nchunks, F_VERIFY, s, src_stride, nullptr, 0,
       chunk_bytes, status);
   return mc_last_launch();
