@@ -59,7 +59,9 @@ MC_DEV McNum map_op(McNum x, int d, int t1, int t2, int a, const McNum &s0, cons
 }
 
 // D_/T1_/T2_/A_ >= 0: compile-time dtypes (specialised hot paths); -1: runtime.
-template <int KIND, int D_, int T1_, int T2_, int A_, bool VEC>
+// EPL = elements per lane per step: 4, or 2 when one side is 8-B elements,
+// so that the wide side moves one lane-contiguous 16-B vector per lane.
+template <int KIND, int D_, int T1_, int T2_, int A_, bool VEC, int EPL = 4>
 __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ src,
                                                   uint8_t *__restrict__ dst, size_t n,
                                                   MapParams prm) {
@@ -69,7 +71,24 @@ __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ sr
   const int a = A_ >= 0 ? A_ : prm.a;
   const int ss = mc_itemsize(d), ds = mc_itemsize(a);
   const size_t base = (size_t)blockIdx.x * ELEMS_PER_BLOCK;
-  if constexpr (VEC) {
+  if constexpr (VEC && EPL == 2) {
+#pragma unroll
+    for (int s = 0; s < 2 * STEPS; ++s) {
+      const size_t i0 = base + (size_t)s * 2 * MC_BLOCK + 2 * (size_t)threadIdx.x;
+      if (i0 + 2 <= n) {
+        uint64_t e[2], o[2];
+        mc_load2(src + i0 * ss, ss, e);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          o[k] = mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e[k], d), d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a);
+        mc_store2(dst + i0 * ds, ds, o);
+      } else if (i0 < n) {
+        mc_store_elem(dst, i0, ds,
+                      mc_num_to_bits(map_op<KIND>(mc_num_from_bits(mc_load_elem(src, i0, ss), d),
+                                                  d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a));
+      }
+    }
+  } else if constexpr (VEC) {
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
       const size_t i0 = base + (size_t)s * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
@@ -227,6 +246,14 @@ static int launch_map(const void *src, void *dst, size_t n, const MapParams &p, 
     k_map<KIND, MC_I2, MC_F8, MC_F8, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
   } else if (KIND == K_QUANTIZE && vec && p.d == MC_F4 && p.a == MC_F4) {
     k_map<KIND, MC_F4, MC_F4, MC_F4, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (KIND == K_CAST && vec && p.d == MC_F4 && p.a == MC_F8) {  // AsType / Quantize decode
+    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_F8, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (KIND == K_CAST && vec && p.d == MC_F8 && p.a == MC_F4) {
+    k_map<KIND, MC_F8, MC_F8, MC_F8, MC_F4, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (KIND == K_QUANTIZE && vec && p.d == MC_F8 && p.a == MC_F4) {
+    k_map<KIND, MC_F8, MC_F8, MC_F8, MC_F4, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  } else if (vec && (mc_itemsize(p.d) == 8 || mc_itemsize(p.a) == 8)) {
+    k_map<KIND, -1, -1, -1, -1, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
   } else if (vec) {
     k_map<KIND, -1, -1, -1, -1, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
   } else {

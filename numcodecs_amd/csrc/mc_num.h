@@ -213,6 +213,38 @@ MC_DEV void mc_load4(const uint8_t *p, int size, uint64_t (&e)[4]) {
     } break;
   }
 }
+// 2 consecutive elements (2*size bytes, 2*size-aligned) as one vector access
+MC_DEV void mc_load2(const uint8_t *p, int size, uint64_t (&e)[2]) {
+  switch (size) {
+    case 1: {
+      const uint32_t w = *reinterpret_cast<const uint16_t *>(p);
+      e[0] = w & 0xffu; e[1] = w >> 8;
+    } break;
+    case 2: {
+      const uint32_t w = mc_ld4<false>(p);
+      e[0] = w & 0xffffu; e[1] = w >> 16;
+    } break;
+    case 4: {
+      const mc_u32x2 w = mc_ld8<false>(p);
+      e[0] = w.x; e[1] = w.y;
+    } break;
+    default: {
+      const mc_u32x4 a = mc_ld16<false>(p);
+      e[0] = ((uint64_t)a.y << 32) | a.x; e[1] = ((uint64_t)a.w << 32) | a.z;
+    } break;
+  }
+}
+MC_DEV void mc_store2(uint8_t *p, int size, const uint64_t (&e)[2]) {
+  switch (size) {
+    case 1: *reinterpret_cast<uint16_t *>(p) = (uint16_t)((e[0] & 0xff) | ((e[1] & 0xff) << 8)); break;
+    case 2: mc_st4<false>(p, (uint32_t)((e[0] & 0xffff) | ((e[1] & 0xffff) << 16))); break;
+    case 4: mc_st8<false>(p, mc_u32x2{(uint32_t)e[0], (uint32_t)e[1]}); break;
+    default:
+      mc_st16<false>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1], (uint32_t)(e[1] >> 32)});
+      break;
+  }
+}
+
 MC_DEV void mc_store4(uint8_t *p, int size, const uint64_t (&e)[4]) {
   switch (size) {
     case 1:
