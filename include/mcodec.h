@@ -280,8 +280,9 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize,
 /* mc_fso_delta_shuffle_decode with an explicit decode schedule: 0 default,
  * 1 three-pass scan, 2 single-pass look-back with an atomic tile counter,
  * 3 single-pass look-back in workgroup order, 4 = 3 with every wait replaced
- * by the data-derived prefix fallback (for tests).  All give identical
- * bytes. */
+ * by the data-derived prefix fallback (for tests), 5 / 6 single-pass
+ * look-back over partitions of 4 / 8 tiles held in registers, 7 = 5 with
+ * the forced fallback (for tests).  All give identical bytes. */
 int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n,
                                         int astype, int dtype, double scale,
                                         double offset, void *workspace,

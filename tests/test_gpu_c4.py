@@ -77,7 +77,7 @@ def test_c4_full_size_fused(device):
     assert hashlib.sha256(dec.view(torch.uint8).cpu().numpy().tobytes()).hexdigest() == full["decoded"]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("dt,at", [("<f4", "<i2"), ("<f8", "<u4"), ("<f4", "<i4")])
 def test_decode_schedules_identical(device, variant, dt, at):
     """Every C4 decode schedule (3-pass scan, look-back with a tile counter,
@@ -86,7 +86,7 @@ def test_decode_schedules_identical(device, variant, dt, at):
     from numcodecs_amd import _ops
     from numcodecs_amd._native import check, lib
 
-    n = 1 << 20 if variant == 4 else 4096 * 300 + 16  # variant 4 is O(tiles^2)
+    n = 1 << 20 if variant in (4, 7) else 4096 * 300 + 16  # variants 4, 7 are O(tiles^2)
     rng = np.random.default_rng(variant)
     x = (1000.0 + rng.uniform(-15, 15, n)).astype(dt)
     codecs = _chain(dt, at, 1000, 1e3 if np.dtype(at).itemsize == 2 else 1e6)
