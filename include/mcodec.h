@@ -27,7 +27,8 @@
  *   mc_fletcher32* ................. fletcher32.pyx:24-57 _fletcher32, :75-89 encode,
  *                                    :91-115 decode; _utils.pxd:11-24 store/load_le32
  *   mc_checksum32_batch /
- *   mc_checksum32_encode_batch ..... checksum32.py:45-88 Checksum32.encode/decode with
+ *   mc_checksum32_encode_batch /
+ *   mc_checksum32_decode_batch ..... checksum32.py:45-88 Checksum32.encode/decode with
  *                                    CRC32 (:95-111, zlib.crc32), Adler32 (:114-130,
  *                                    zlib.adler32), CRC32C (:189-209), JenkinsLookup3
  *                                    (:133-181 over jenkins.pyx:93-325)
@@ -173,6 +174,24 @@ int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks,
                         size_t chunk_bytes, uint32_t *out_sums,
                         void *workspace, size_t workspace_bytes,
                         mc_stream_t stream);
+/* Fletcher32.encode of every chunk: dst row c = chunk c ++ LE32 checksum
+ * (dst_stride >= chunk_bytes + 4, chunk_bytes >= 1), one pass.  Workspace:
+ * mc_fletcher32_batch_workspace(nchunks, chunk_bytes). */
+int mc_fletcher32_encode_batch(const void *src, size_t src_stride, void *dst,
+                               size_t dst_stride, size_t nchunks,
+                               size_t chunk_bytes, void *workspace,
+                               size_t workspace_bytes, mc_stream_t stream);
+/* Fletcher32.decode of every encoded row (fletcher32.pyx:91-115): rows of
+ * encoded_bytes = payload + LE32 footer.  out_pairs[2c] = fletcher32 of the
+ * payload, out_pairs[2c+1] = the stored footer (the caller compares and
+ * raises); when dst is not NULL the payloads are compacted into dst rows
+ * (dst_stride >= encoded_bytes - 4) in the same pass.  Workspace:
+ * mc_fletcher32_batch_workspace(nchunks, encoded_bytes - 4). */
+int mc_fletcher32_decode_batch(const void *src, size_t src_stride, void *dst,
+                               size_t dst_stride, size_t nchunks,
+                               size_t encoded_bytes, uint32_t *out_pairs,
+                               void *workspace, size_t workspace_bytes,
+                               mc_stream_t stream);
 
 /* ---- fused chunk pipelines (Zarr filter chain -> checksum) ------------- */
 /* Workspace for the two calls below. */
@@ -252,6 +271,20 @@ int mc_checksum32_encode_batch(int kind, const void *src, size_t src_stride,
                                int location, uint32_t *out_sums,
                                void *workspace, size_t workspace_bytes,
                                mc_stream_t stream);
+/* Checksum32.decode of every encoded row (checksum32.py:64-88): rows of
+ * encoded_bytes (payload + 4 checksum bytes at `location`).  Writes the
+ * checksum of every payload to out_sums and the stored LE32 value to
+ * out_stored (the caller compares them and raises), and, when dst is not
+ * NULL, the payloads compacted into dst rows (dst_stride >= encoded_bytes - 4)
+ * in the same pass over the encoded bytes (Jenkins: one hipMemcpy2DAsync).
+ * Workspace: mc_checksum32_workspace(kind, nchunks, encoded_bytes - 4). */
+int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride,
+                               void *dst, size_t dst_stride, size_t nchunks,
+                               size_t encoded_bytes, uint32_t init,
+                               const void *prefix, size_t prefix_bytes,
+                               int location, uint32_t *out_sums,
+                               uint32_t *out_stored, void *workspace,
+                               size_t workspace_bytes, mc_stream_t stream);
 
 /* ---- PackBits (packbits.py:33-82) --------------------------------------- */
 /* encode n bools (any nonzero byte is True) into dst[0] = padding bits

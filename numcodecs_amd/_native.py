@@ -100,6 +100,8 @@ _SIGNATURES = {
     "mc_fletcher32_verify": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_batch_workspace": [_c_size, _c_size],
     "mc_fletcher32_batch": [_c_vp, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_shuffle_fletcher32_workspace": [_c_size, _c_size, _c_size],
     "mc_shuffle_fletcher32_encode_batch": [
         _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_size, _c_vp, _c_size, _c_vp,
@@ -123,6 +125,10 @@ _SIGNATURES = {
     "mc_checksum32_encode_batch": [
         _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_int,
         _c_vp, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_checksum32_decode_batch": [
+        _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_int,
+        _c_vp, _c_vp, _c_vp, _c_size, _c_vp,
     ],
     "mc_packbits": [_c_vp, _c_vp, _c_size, _c_vp],
     "mc_blosc_filter": [_c_vp, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],

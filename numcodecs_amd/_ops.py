@@ -255,6 +255,27 @@ def checksum32_encode(kind, src, src_stride, dst, dst_stride, nchunks, nbytes, i
               "mc_checksum32_encode_batch")
 
 
+def checksum32_decode(kind, src, src_stride, dst, dst_stride, nchunks, encoded_bytes, init, location,
+                      prefix=None):
+    """Checksum32.decode of `nchunks` encoded rows: (sums, stored) device int32[nchunks]
+    (uint32 bit patterns); the payloads land compacted in dst rows when dst is given."""
+    _native.require_device()
+    sums = torch.empty(max(nchunks, 1), dtype=torch.int32, device=src.device)
+    stored = torch.empty(max(nchunks, 1), dtype=torch.int32, device=src.device)
+    with _guard(src):
+        pre = _prefix_dev(prefix, src)
+        ws = workspace(lib.mc_checksum32_workspace(kind, nchunks, encoded_bytes - 4), src)
+        check(lib.mc_checksum32_decode_batch(kind, src.data_ptr(), src_stride,
+                                             dst.data_ptr() if dst is not None else None, dst_stride,
+                                             nchunks, encoded_bytes, init & 0xFFFFFFFF,
+                                             pre.data_ptr() if pre is not None else None,
+                                             pre.numel() if pre is not None else 0, location,
+                                             sums.data_ptr(), stored.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             stream(src)),
+              "mc_checksum32_decode_batch")
+    return sums[:nchunks], stored[:nchunks]
+
+
 def packbits(src, dst, n) -> None:
     _native.require_device()
     with _guard(dst):

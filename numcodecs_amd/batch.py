@@ -42,6 +42,9 @@ __all__ = [
     "host_pipeline",
     "checksum32_chunks",
     "checksum32_encode_chunks",
+    "checksum32_decode_chunks",
+    "fletcher32_encode_chunks",
+    "fletcher32_decode_chunks",
 ]
 
 _CK_KINDS = {
@@ -134,6 +137,48 @@ def fletcher32_chunks(chunks, nbytes=None) -> torch.Tensor:
     return res.to(torch.int64) & 0xFFFFFFFF
 
 
+def fletcher32_encode_chunks(chunks, out=None):
+    """Fletcher32.encode of every chunk in one pass (fletcher32.pyx:75-89):
+    the [B, row_bytes + 4] batch of payload ++ LE32 checksum (or `out`)."""
+    rows = _as_rows(chunks)
+    b, n = rows.shape
+    if n == 0:  # the reference indexes b_mv[0] of an empty view
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    out = torch.empty((b, n + 4), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if out.shape[0] != b or out.shape[1] < n + 4:
+        raise ValueError("output rows must hold chunk_bytes + 4 bytes")
+    if b:
+        _native.require_device()
+        with torch.cuda.device(rows.device):
+            ws = _ops.workspace(lib.mc_fletcher32_batch_workspace(b, n), rows)
+            check(lib.mc_fletcher32_encode_batch(rows.data_ptr(), rows.stride(0), out.data_ptr(), out.stride(0), b, n,
+                                                 ws.data_ptr(), ws.numel(), _ops.stream(rows)),
+                  "mc_fletcher32_encode_batch")
+    return out
+
+
+def fletcher32_decode_chunks(chunks):
+    """Fletcher32.decode of every encoded row (payload + LE32 footer) in one
+    pass: ``(payloads, sums, stored)`` -- the payloads compacted into a fresh
+    contiguous [B, row_bytes - 4] batch, the computed and the stored checksums
+    (device int32 [B], uint32 bit patterns).  The caller compares and raises
+    (fletcher32.pyx:106-113); nothing here syncs the host."""
+    rows = _as_rows(chunks)
+    b, m = rows.shape
+    if m < 4:
+        raise IndexError("Out of bounds on buffer access (axis 0)")
+    out = torch.empty((b, m - 4), dtype=torch.uint8, device=rows.device)
+    pairs = torch.empty((max(b, 1), 2), dtype=torch.int32, device=rows.device)
+    if b:
+        _native.require_device()
+        with torch.cuda.device(rows.device):
+            ws = _ops.workspace(lib.mc_fletcher32_batch_workspace(b, m - 4), rows)
+            check(lib.mc_fletcher32_decode_batch(rows.data_ptr(), rows.stride(0), out.data_ptr(), m - 4, b, m,
+                                                 pairs.data_ptr(), ws.data_ptr(), ws.numel(), _ops.stream(rows)),
+                  "mc_fletcher32_decode_batch")
+    return out, pairs[:b, 0], pairs[:b, 1]
+
+
 def checksum32_chunks(chunks, codec_id, nbytes=None, value=None, prefix=None) -> torch.Tensor:
     """`codec_id` checksum ('crc32', 'crc32c', 'adler32', 'jenkins_lookup3')
     of every chunk (first `nbytes` of each row), one launch; int64 [B].
@@ -168,6 +213,31 @@ def checksum32_encode_chunks(chunks, codec_id, location=None, out=None, value=No
         _ops.checksum32_encode(kind, rows, rows.stride(0), out, out.stride(0), b, n,
                                default if value is None else value, loc, prefix)
     return out
+
+
+def checksum32_decode_chunks(chunks, codec_id, location=None, value=None, prefix=None):
+    """Checksum32.decode of every encoded row in one pass: returns
+    ``(payloads, sums, stored)`` -- the [B, row_bytes - 4] payloads compacted
+    into a fresh contiguous batch, the computed checksums and the stored ones
+    (device int32 [B], uint32 bit patterns).  The caller compares and raises
+    (checksum32.py:79-87); nothing here syncs the host."""
+    kind, default = _CK_KINDS[codec_id]
+    if location is None:
+        location = "end" if codec_id in ("crc32c", "jenkins_lookup3") else "start"
+    if location not in ("start", "end") or (codec_id == "jenkins_lookup3" and location != "end"):
+        raise ValueError(f"Invalid checksum location: {location}")
+    rows = _as_rows(chunks)
+    b, m = rows.shape
+    if m < 4:
+        raise ValueError("Input buffer is too short to contain a 32-bit checksum.")
+    out = torch.empty((b, m - 4), dtype=torch.uint8, device=rows.device)
+    if b == 0:
+        z = torch.empty(0, dtype=torch.int32, device=rows.device)
+        return out, z, z
+    loc = _native.MC_CK_START if location == "start" else _native.MC_CK_END
+    sums, stored = _ops.checksum32_decode(kind, rows, rows.stride(0), out if m > 4 else None, m - 4, b, m,
+                                          default if value is None else value, loc, prefix)
+    return out, sums, stored
 
 
 def shuffle_fletcher32_encode_chunks(chunks, elementsize, out=None):

@@ -300,6 +300,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
   }
 }
 
+MC_DEV uint32_t load_le32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
 MC_DEV void store_le32(uint8_t *p, uint32_t v) {
   p[0] = (uint8_t)v;
   p[1] = (uint8_t)(v >> 8);
@@ -312,9 +316,11 @@ MC_DEV void store_le32(uint8_t *p, uint32_t v) {
 template <int KIND, int K>
 __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
     const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
-    uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride) {
+    uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride,
+    const uint8_t *__restrict__ stored, size_t stored_stride, uint32_t *__restrict__ stored_out) {
   __shared__ uint64_t red[2][MC_BLOCK / 64];
   const size_t c = blockIdx.x;
+  if (stored_out && threadIdx.x == 0) stored_out[c] = load_le32(stored + c * stored_stride);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t lo = tiles_per_chunk * threadIdx.x / MC_BLOCK;
   const size_t hi = tiles_per_chunk * (threadIdx.x + 1) / MC_BLOCK;
@@ -401,9 +407,12 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
                                                 const uint8_t *__restrict__ prefix, size_t plen,
                                                 uint32_t *__restrict__ out,
                                                 uint8_t *__restrict__ footer,
-                                                size_t footer_stride) {
+                                                size_t footer_stride,
+                                                const uint8_t *__restrict__ stored,
+                                                uint32_t *__restrict__ stored_out) {
   const size_t ci = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= nchunks) return;
+  if (stored_out) stored_out[ci] = load_le32(stored + ci * src_stride);
   const uint8_t *s = src + ci * src_stride;
   const size_t L = plen + n;
   uint32_t a, b, c;
@@ -537,6 +546,7 @@ void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n
   }
   const int ald = align_class(d, ds, nchunks);
   if (als == 2 && ald == 2) launch_tiles<KIND, K, true, 2, 2>(s, ss, d, ds, n, tpc, total, parts, st);
+  else if (als == 1 && ald == 2) launch_tiles<KIND, K, true, 1, 2>(s, ss, d, ds, n, tpc, total, parts, st);
   else if (als == 2 && ald == 1) launch_tiles<KIND, K, true, 2, 1>(s, ss, d, ds, n, tpc, total, parts, st);
   else if (als >= 1 && ald >= 1) launch_tiles<KIND, K, true, 1, 1>(s, ss, d, ds, n, tpc, total, parts, st);
   else launch_tiles<KIND, K, true, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
@@ -544,8 +554,8 @@ void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n
 
 template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
-                  uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, void *ws,
-                  size_t ws_bytes, hipStream_t st) {
+                  uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
+                  uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st) {
   const int K = ck_k(n);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
@@ -555,8 +565,8 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
 #define MC_CK_CASE(KK)                                                                         \
   case KK:                                                                                     \
     dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, st);                        \
-    k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(parts, tpc, n, init, out,  \
-                                                                    footer, fs);               \
+    k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                           \
+        parts, tpc, n, init, out, footer, fs, stored, ss, stored_out);                         \
     break;
     MC_CK_CASE(1)
     MC_CK_CASE(4)
@@ -571,21 +581,26 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
 
 int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks,
                 size_t n, uint32_t init, const uint8_t *prefix, size_t plen, uint32_t *out,
-                uint8_t *footer, size_t fs, void *ws, size_t ws_bytes, hipStream_t st) {
+                uint8_t *footer, size_t fs, const uint8_t *stored, uint32_t *stored_out, void *ws,
+                size_t ws_bytes, hipStream_t st) {
   switch (kind) {
     case MC_CK_CRC32:
-      return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+      return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
+                                    ws, ws_bytes, st);
     case MC_CK_CRC32C:
-      return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+      return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
+                                     ws, ws_bytes, st);
     case MC_CK_ADLER32:
-      return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, ws, ws_bytes, st);
+      return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
+                                    ws, ws_bytes, st);
     case MC_CK_JENKINS: {
       if (d && n) {
         const hipError_t e = hipMemcpy2DAsync(d, ds, s, ss, n, nchunks, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return mc_hip_status(e);
       }
       const unsigned grid = (unsigned)((nchunks + 63) / 64);
-      k_jenkins<<<grid, 64, 0, st>>>(s, ss, nchunks, n, init, prefix, plen, out, footer, fs);
+      k_jenkins<<<grid, 64, 0, st>>>(s, ss, nchunks, n, init, prefix, plen, out, footer, fs, stored,
+                                     stored_out);
       return mc_last_launch();
     }
     default:
@@ -616,7 +631,8 @@ int mc_checksum32_batch(int kind, const void *src, size_t src_stride, size_t nch
   if (nchunks > 0x7fffffffu) return MC_EINVAL;
   return ck_dispatch(kind, static_cast<const uint8_t *>(src), src_stride, nullptr, 0, nchunks,
                      chunk_bytes, init, static_cast<const uint8_t *>(prefix), prefix_bytes,
-                     out_sums, nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream);
+                     out_sums, nullptr, 0, nullptr, nullptr, workspace, workspace_bytes,
+                     (hipStream_t)stream);
 }
 
 int mc_checksum32_encode_batch(int kind, const void *src, size_t src_stride, void *dst,
@@ -635,8 +651,28 @@ int mc_checksum32_encode_batch(int kind, const void *src, size_t src_stride, voi
   uint8_t *footer = location == MC_CK_START ? d : d + chunk_bytes;
   return ck_dispatch(kind, static_cast<const uint8_t *>(src), src_stride, payload, dst_stride,
                      nchunks, chunk_bytes, init, static_cast<const uint8_t *>(prefix),
-                     prefix_bytes, out_sums, footer, dst_stride, workspace, workspace_bytes,
-                     (hipStream_t)stream);
+                     prefix_bytes, out_sums, footer, dst_stride, nullptr, nullptr, workspace,
+                     workspace_bytes, (hipStream_t)stream);
+}
+
+int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride, void *dst,
+                               size_t dst_stride, size_t nchunks, size_t encoded_bytes,
+                               uint32_t init, const void *prefix, size_t prefix_bytes,
+                               int location, uint32_t *out_sums, uint32_t *out_stored,
+                               void *workspace, size_t workspace_bytes, mc_stream_t stream) {
+  if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
+  if (nchunks == 0) return MC_OK;
+  if (encoded_bytes < 4 || !src || !out_sums || !out_stored) return MC_EINVAL;
+  const size_t n = encoded_bytes - 4;
+  if (nchunks > 1 && (src_stride < encoded_bytes || (dst && dst_stride < n))) return MC_EINVAL;
+  if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
+  if (nchunks > 0x7fffffffu) return MC_EINVAL;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  const uint8_t *payload = location == MC_CK_START ? s + 4 : s;
+  const uint8_t *stored = location == MC_CK_START ? s : s + n;
+  return ck_dispatch(kind, payload, src_stride, static_cast<uint8_t *>(dst), dst_stride, nchunks, n,
+                     init, static_cast<const uint8_t *>(prefix), prefix_bytes, out_sums, nullptr, 0,
+                     stored, out_stored, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -114,11 +114,30 @@ MC_DEV uint32_t load_le32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// 16-B vector access; AL = 2: 16-B aligned (nontemporal), 1: 4-B aligned
+// (global_load/store_dwordx4 at dword alignment: rows of chunk_bytes + 4)
+template <int AL>
+MC_DEV mc_u32x4 f32_ld(const uint8_t *p) {
+  if constexpr (AL == 2) {
+    return mc_ld16<true>(p);
+  } else {
+    mc_u32x4 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
+    return v;
+  }
+}
+template <int AL>
+MC_DEV void f32_st(uint8_t *p, mc_u32x4 v) {
+  if constexpr (AL == 2) mc_st16<true>(p, v);
+  else __builtin_memcpy(__builtin_assume_aligned(p, 4), &v, 16);
+}
+
 // ---------------------------------------------------------------------------
 // checksum (optionally fused with a copy) over slices of chunks
 // block = (chunk c, slice sl); partials[block] = {S1, S2, nz}
+// AL: alignment class of src/dst rows (above); 0 = bytes only
 // ---------------------------------------------------------------------------
-template <bool COPY, bool VEC>
+template <bool COPY, int AL>
 __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials) {
@@ -127,7 +146,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
   const uint8_t *s = src + c * src_stride;
   uint8_t *d = COPY ? dst + c * dst_stride : nullptr;
   const uint64_t nwords = (nbytes + 1) / 2;
-  const size_t nvec = VEC ? nbytes / 16 : 0;
+  const size_t nvec = AL ? nbytes / 16 : 0;
   const size_t v_lo = nvec * sl / nslices, v_hi = nvec * (sl + 1) / nslices;
   F32Part p;
   part_init(p);
@@ -137,8 +156,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     uint32_t cw = (uint32_t)((nwords - 8 * (uint64_t)v) % M);
     constexpr uint32_t STEP = (8u * MC_BLOCK) % M;
     for (; v < v_hi; v += MC_BLOCK) {
-      const mc_u32x4 x = mc_ld16<true>(s + v * 16);
-      if constexpr (COPY) mc_st16<true>(d + v * 16, x);
+      const mc_u32x4 x = f32_ld<AL>(s + v * 16);
+      if constexpr (COPY) f32_st<AL>(d + v * 16, x);
       part_vec(p, x, cw);
       cw = cw >= STEP ? cw - STEP : cw + M - STEP;
     }
@@ -307,6 +326,35 @@ static size_t partials_bytes(size_t nchunks, unsigned nslices) {
   return nchunks * (size_t)nslices * 3 * sizeof(uint32_t);
 }
 
+static int align_class(const void *p, size_t stride, size_t nchunks) {
+  const uintptr_t a = (uintptr_t)p | (nchunks > 1 ? stride : 0);
+  return a % 16 == 0 ? 2 : a % 4 == 0 ? 1 : 0;
+}
+
+static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
+                           size_t nchunks, size_t nbytes, unsigned nsl, uint32_t *partials,
+                           hipStream_t st) {
+  int al = align_class(src, src_stride, nchunks);
+  if (dst) {
+    const int ad = align_class(dst, dst_stride, nchunks);
+    al = al < ad ? al : ad;
+  }
+  const unsigned grid = (unsigned)(nchunks * nsl);
+#define MC_F32_LAUNCH(CP, AL)                                                                   \
+  k_f32_partial<CP, AL><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, \
+                                                   partials)
+  if (dst) {
+    if (al == 2) MC_F32_LAUNCH(true, 2);
+    else if (al == 1) MC_F32_LAUNCH(true, 1);
+    else MC_F32_LAUNCH(true, 0);
+  } else {
+    if (al == 2) MC_F32_LAUNCH(false, 2);
+    else if (al == 1) MC_F32_LAUNCH(false, 1);
+    else MC_F32_LAUNCH(false, 0);
+  }
+#undef MC_F32_LAUNCH
+}
+
 // standalone driver: checksum (+ optional copy) of nchunks chunks, then finalize
 static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                    size_t nchunks, size_t nbytes, int mode, uint32_t *out, void *ws,
@@ -314,17 +362,10 @@ static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t d
   const unsigned nsl = slices_for(nbytes, nchunks);
   if (!ws || ws_bytes < partials_bytes(nchunks, nsl)) return MC_ENOSPC;
   uint32_t *partials = static_cast<uint32_t *>(ws);
-  const bool copy = dst != nullptr && mode != F_VERIFY;
-  const bool vec = ((uintptr_t)src % 16 == 0) && (src_stride % 16 == 0 || nchunks == 1) &&
-                   (!copy || (((uintptr_t)dst % 16 == 0) && (dst_stride % 16 == 0 || nchunks == 1)));
-  const size_t grid = nchunks * nsl;
-  if (copy) {
-    if (vec) k_f32_partial<true, true><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, partials);
-    else k_f32_partial<true, false><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, partials);
-  } else {
-    if (vec) k_f32_partial<false, true><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, nullptr, 0, nbytes, nsl, partials);
-    else k_f32_partial<false, false><<<(unsigned)grid, MC_BLOCK, 0, st>>>(src, src_stride, nullptr, 0, nbytes, nsl, partials);
-  }
+  // F_FOOTER copies the payload in front of its footer; F_VERIFY with a dst
+  // compacts the payloads out of the encoded rows (the decode pass)
+  const bool copy = dst != nullptr;
+  launch_partial(src, src_stride, copy ? dst : nullptr, dst_stride, nchunks, nbytes, nsl, partials, st);
   int rc = mc_last_launch();
   if (rc != MC_OK) return rc;
   k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride,
@@ -394,6 +435,31 @@ int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks, size_t c
                  out_sums, workspace, workspace_bytes, st);
 }
 
+int mc_fletcher32_encode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                               size_t nchunks, size_t chunk_bytes, void *workspace,
+                               size_t workspace_bytes, mc_stream_t stream) {
+  if (nchunks == 0) return MC_OK;
+  if (!src || !dst || chunk_bytes == 0) return MC_EINVAL;
+  if (nchunks > 1 && (src_stride < chunk_bytes || dst_stride < chunk_bytes + 4)) return MC_EINVAL;
+  if (nchunks > 0x7fffffffu) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), src_stride, static_cast<uint8_t *>(dst), dst_stride,
+                 nchunks, chunk_bytes, F_FOOTER, nullptr, workspace, workspace_bytes,
+                 (hipStream_t)stream);
+}
+
+int mc_fletcher32_decode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                               size_t nchunks, size_t encoded_bytes, uint32_t *out_pairs,
+                               void *workspace, size_t workspace_bytes, mc_stream_t stream) {
+  if (nchunks == 0) return MC_OK;
+  if (!src || !out_pairs || encoded_bytes < 4) return MC_EINVAL;
+  const size_t n = encoded_bytes - 4;
+  if (nchunks > 1 && (src_stride < encoded_bytes || (dst && dst_stride < n))) return MC_EINVAL;
+  if (nchunks > 0x7fffffffu) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), src_stride, n ? static_cast<uint8_t *>(dst) : nullptr,
+                 dst_stride, nchunks, n, F_VERIFY, out_pairs, workspace, workspace_bytes,
+                 (hipStream_t)stream);
+}
+
 size_t mc_fletcher32_batch_workspace(size_t nchunks, size_t chunk_bytes) {
   return partials_bytes(nchunks, slices_for(chunk_bytes, nchunks));
 }
@@ -430,9 +496,7 @@ int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void 
     if (rc != MC_OK) return rc;
     const unsigned nsl = slices_for(chunk_bytes, nchunks);
     uint32_t *partials = static_cast<uint32_t *>(workspace);
-    const bool vec = ((uintptr_t)d % 16 == 0) && (dst_stride % 16 == 0);
-    if (vec) k_f32_partial<false, true><<<(unsigned)(nchunks * nsl), MC_BLOCK, 0, st>>>(d, dst_stride, nullptr, 0, chunk_bytes, nsl, partials);
-    else k_f32_partial<false, false><<<(unsigned)(nchunks * nsl), MC_BLOCK, 0, st>>>(d, dst_stride, nullptr, 0, chunk_bytes, nsl, partials);
+    launch_partial(d, dst_stride, nullptr, 0, nchunks, chunk_bytes, nsl, partials, st);
     rc = mc_last_launch();
     if (rc != MC_OK) return rc;
     k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(

@@ -451,6 +451,31 @@ def test_batch_shuffle_and_checksums(device):
     assert [int(v) for v in sums] == [oracle.fletcher32(xh[c]) for c in range(16)]
 
 
+def test_fletcher32_decode_batches(device):
+    """mc_fletcher32_encode_batch / mc_fletcher32_decode_batch: payloads compacted out of rows of every
+    alignment (stride payload + 4), computed vs stored footers, a corrupted
+    row (fletcher32.pyx:91-115 per row)."""
+    for b, n in ((1, 4096), (37, 1000), (16, 65536 + 12), (9, (1 << 20) + 6), (300, 4096 * 3 + 1), (5, 1)):
+        for pad in (0, 3, 16):
+            rows = torch.randint(0, 256, (b, n + pad), dtype=torch.uint8, device=device)[:, :n]
+            host = rows.cpu().numpy()
+            wide = torch.zeros((b, n + 4 + pad), dtype=torch.uint8, device=device)
+            batch.fletcher32_encode_chunks(rows, out=wide)  # mc_fletcher32_encode_batch into padded rows
+            enc = wide[:, : n + 4].cpu().numpy()
+            for i in range(b):
+                assert enc[i].tobytes() == oracle.fletcher32_encode(host[i]), (b, n, pad, i)
+            bad = min(b - 1, 2)
+            wide[bad, n // 2] ^= 0x20
+            payload, sums, stored = batch.fletcher32_decode_chunks(wide[:, : n + 4])
+            exp = host.copy()
+            exp[bad, n // 2] ^= 0x20
+            assert payload.is_contiguous() and np.array_equal(payload.cpu().numpy(), exp), (b, n, pad)
+            assert sums.cpu().numpy().view("<u4").tolist() == [oracle.fletcher32(exp[i]) for i in range(b)]
+            assert stored.cpu().numpy().view("<u4").tolist() == [oracle.fletcher32(host[i]) for i in range(b)]
+            mism = (sums != stored).cpu().numpy()
+            assert mism[bad] and not mism[[i for i in range(b) if i != bad]].any(), (b, n, pad)
+
+
 def test_pipeline_fusion_matches_sequential(device):
     x = torch.from_numpy(RNG.standard_normal(4096 * 40).astype("f4")).to(device)
     pipe = batch.FilterPipeline([BitRound(10), Shuffle(4), Fletcher32()])

@@ -145,6 +145,37 @@ def test_checksum_batches(device, codec_id):
             assert torch.equal(torch.as_tensor(codec.decode(enc[i])).to(device), rows[i])
 
 
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32", "jenkins_lookup3"])
+def test_checksum_decode_batches(device, codec_id):
+    """mc_checksum32_decode_batch: the payloads compacted, the computed and
+    stored checksums, for both locations, row strides of every alignment and
+    corrupted rows (checksum32.py:64-88 applied per row)."""
+    ref = {**REF, "jenkins_lookup3": oracle.jenkins_lookup3}[codec_id]
+    locs = ["end"] if codec_id == "jenkins_lookup3" else ["start", "end"]
+    for loc in locs:
+        for b, n in ((1, 4096), (37, 1000), (64, 65536 + 12), (9, (1 << 20) + 5), (300, 4096 * 3 + 1), (5, 0)):
+            for pad in (0, 3, 16):
+                rows = torch.randint(0, 256, (b, n + pad), dtype=torch.uint8, device=device)[:, :n]
+                enc = batch.checksum32_encode_chunks(rows, codec_id, location=loc)
+                wide = torch.zeros((b, n + 4 + pad), dtype=torch.uint8, device=device)
+                wide[:, : n + 4] = enc
+                bad = min(b - 1, 3)
+                if n:
+                    wide[bad, (n + 4) // 2] ^= 0x40
+                payload, sums, stored = batch.checksum32_decode_chunks(wide[:, : n + 4], codec_id, location=loc)
+                exp = rows.clone()
+                if n:
+                    exp[bad, (n + 4) // 2 - (4 if loc == "start" else 0)] ^= 0x40
+                assert payload.is_contiguous() and torch.equal(payload, exp), (loc, b, n, pad)
+                host = exp.cpu().numpy()
+                assert (sums.cpu().numpy().view("<u4").tolist() == [ref(host[i]) for i in range(b)]), (loc, b, n, pad)
+                want = enc.cpu().numpy()[:, :4] if loc == "start" else enc.cpu().numpy()[:, n:]
+                assert stored.cpu().numpy().view("<u4").tolist() == np.ascontiguousarray(want).view("<u4")[:, 0].tolist()
+                mismatch = (sums != stored).cpu().numpy()
+                assert mismatch[bad] == bool(n)
+                assert not mismatch[[i for i in range(b) if i != bad]].any()
+
+
 def test_packbits_fixtures_and_sizes(device):
     for arr, _j, _config, enc in fixture_cases("packbits"):
         assert PackBits().encode(arr).tobytes() == enc
