@@ -494,8 +494,12 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// Tuning knobs (read once): MCODEC_CK_K = tile size in STEP units for chunks
-// of >= 64 KiB (4, 8 or 16), MCODEC_CK_GRID = persistent grid cap.
+// Tuning knobs (read once): MCODEC_CK_K / MCODEC_CK_KCOPY = tile size in STEP
+// units for chunks of >= 64 KiB (4, 8 or 16) without / with the fused payload
+// copy, MCODEC_CK_GRID / MCODEC_CK_GRID_COPY = persistent grid caps.  Defaults
+// from the sweep on 64 x 4 MiB: the checksum alone is best with
+// 64 KiB tiles, the copying passes (encode, decode) with 32 KiB tiles and
+// 1024 workgroups (CRC32 decode 139 -> 120 us).
 inline int ck_env(const char *name, int def) {
   const char *v = getenv(name);
   return v ? atoi(v) : def;
@@ -507,16 +511,34 @@ inline int ck_kbig() {
   }();
   return k;
 }
-inline unsigned ck_grid_cap() {
+inline int ck_kcopy() {
+  static const int k = [] {
+    const int e = ck_env("MCODEC_CK_KCOPY", 8);
+    return (e == 4 || e == 8 || e == 16) ? e : 8;
+  }();
+  return k;
+}
+inline unsigned ck_grid_cap(bool copy) {
   static const unsigned g = [] {
     const int e = ck_env("MCODEC_CK_GRID", 2048);
     return e > 0 ? (unsigned)e : 2048u;
   }();
-  return g;
+  static const unsigned gc = [] {
+    const int e = ck_env("MCODEC_CK_GRID_COPY", 1024);
+    return e > 0 ? (unsigned)e : 1024u;
+  }();
+  return copy ? gc : g;
 }
 
 // tile size (in STEP units) for a chunk: K = 1 below 64 KiB
-inline int ck_k(size_t n) { return n < (size_t)16 * STEP ? 1 : ck_kbig(); }
+inline int ck_k(size_t n, bool copy) {
+  return n < (size_t)16 * STEP ? 1 : copy ? ck_kcopy() : ck_kbig();
+}
+// the workspace covers either pass
+inline int ck_k_ws(size_t n) {
+  const int a = ck_k(n, false), b = ck_k(n, true);
+  return a < b ? a : b;
+}
 inline size_t ck_tiles(size_t n, int K) {
   const size_t tb = (size_t)K * STEP;
   return n ? (n + tb - 1) / tb : 1;
@@ -529,7 +551,8 @@ inline int align_class(const void *p, size_t stride, size_t nchunks) {
 template <int KIND, int K, bool COPY, int ALS, int ALD>
 void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
                   size_t total, uint32_t *parts, hipStream_t st) {
-  const unsigned grid = (unsigned)(total < ck_grid_cap() ? total : ck_grid_cap());
+  const unsigned cap = ck_grid_cap(COPY);
+  const unsigned grid = (unsigned)(total < cap ? total : cap);
   k_ck_tiles<KIND, K, COPY, ALS, ALD><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts);
 }
 
@@ -556,7 +579,7 @@ template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
                   uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
                   uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st) {
-  const int K = ck_k(n);
+  const int K = ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;
@@ -616,7 +639,7 @@ extern "C" {
 
 size_t mc_checksum32_workspace(int kind, size_t nchunks, size_t chunk_bytes) {
   if (!valid_kind(kind) || kind == MC_CK_JENKINS) return 0;
-  const size_t tpc = ck_tiles(chunk_bytes, ck_k(chunk_bytes));
+  const size_t tpc = ck_tiles(chunk_bytes, ck_k_ws(chunk_bytes));
   return tpc * nchunks * (kind == MC_CK_ADLER32 ? 8 : 4);
 }
 

@@ -137,7 +137,7 @@ MC_DEV void f32_st(uint8_t *p, mc_u32x4 v) {
 // block = (chunk c, slice sl); partials[block] = {S1, S2, nz}
 // AL: alignment class of src/dst rows (above); 0 = bytes only
 // ---------------------------------------------------------------------------
-template <bool COPY, int AL>
+template <bool COPY, int AL, int F32_UNROLL>
 __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials) {
@@ -155,6 +155,18 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     // weight of the vector's first word, stepped by 8*MC_BLOCK words per iteration
     uint32_t cw = (uint32_t)((nwords - 8 * (uint64_t)v) % M);
     constexpr uint32_t STEP = (8u * MC_BLOCK) % M;
+    // F32_UNROLL vectors in flight per thread before any is consumed
+    for (; v + (F32_UNROLL - 1) * MC_BLOCK < v_hi; v += F32_UNROLL * MC_BLOCK) {
+      mc_u32x4 x[F32_UNROLL];
+#pragma unroll
+      for (int j = 0; j < F32_UNROLL; ++j) x[j] = f32_ld<AL>(s + (v + j * MC_BLOCK) * 16);
+#pragma unroll
+      for (int j = 0; j < F32_UNROLL; ++j) {
+        if constexpr (COPY) f32_st<AL>(d + (v + j * MC_BLOCK) * 16, x[j]);
+        part_vec(p, x[j], cw);
+        cw = cw >= STEP ? cw - STEP : cw + M - STEP;
+      }
+    }
     for (; v < v_hi; v += MC_BLOCK) {
       const mc_u32x4 x = f32_ld<AL>(s + v * 16);
       if constexpr (COPY) f32_st<AL>(d + v * 16, x);
@@ -326,6 +338,15 @@ static size_t partials_bytes(size_t nchunks, unsigned nslices) {
   return nchunks * (size_t)nslices * 3 * sizeof(uint32_t);
 }
 
+// MCODEC_F32_UNROLL: vectors in flight per thread in k_f32_partial (1 or 4)
+static int f32_unroll() {
+  static const int u = [] {
+    const char *e = getenv("MCODEC_F32_UNROLL");
+    return e && atoi(e) == 1 ? 1 : 4;
+  }();
+  return u;
+}
+
 static int align_class(const void *p, size_t stride, size_t nchunks) {
   const uintptr_t a = (uintptr_t)p | (nchunks > 1 ? stride : 0);
   return a % 16 == 0 ? 2 : a % 4 == 0 ? 1 : 0;
@@ -340,9 +361,15 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
     al = al < ad ? al : ad;
   }
   const unsigned grid = (unsigned)(nchunks * nsl);
-#define MC_F32_LAUNCH(CP, AL)                                                                   \
-  k_f32_partial<CP, AL><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride, nbytes, nsl, \
-                                                   partials)
+#define MC_F32_LAUNCH(CP, AL)                                                                 \
+  do {                                                                                         \
+    if (f32_unroll() == 4)                                                                     \
+      k_f32_partial<CP, AL, 4><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride,    \
+                                                          nbytes, nsl, partials);              \
+    else                                                                                       \
+      k_f32_partial<CP, AL, 1><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride,    \
+                                                          nbytes, nsl, partials);              \
+  } while (0)
   if (dst) {
     if (al == 2) MC_F32_LAUNCH(true, 2);
     else if (al == 1) MC_F32_LAUNCH(true, 1);
