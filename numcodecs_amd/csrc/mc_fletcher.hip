@@ -116,10 +116,10 @@ MC_DEV uint32_t load_le32(const uint8_t *p) {
 
 // 16-B vector access; AL = 2: 16-B aligned (nontemporal), 1: 4-B aligned
 // (global_load/store_dwordx4 at dword alignment: rows of chunk_bytes + 4)
-template <int AL>
+template <int AL, bool NT = true>
 MC_DEV mc_u32x4 f32_ld(const uint8_t *p) {
   if constexpr (AL == 2) {
-    return mc_ld16<true>(p);
+    return mc_ld16<NT>(p);
   } else {
     mc_u32x4 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
@@ -137,7 +137,7 @@ MC_DEV void f32_st(uint8_t *p, mc_u32x4 v) {
 // block = (chunk c, slice sl); partials[block] = {S1, S2, nz}
 // AL: alignment class of src/dst rows (above); 0 = bytes only
 // ---------------------------------------------------------------------------
-template <bool COPY, int AL, int F32_UNROLL>
+template <bool COPY, int AL, int F32_UNROLL, bool NT>
 __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials) {
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     for (; v + (F32_UNROLL - 1) * MC_BLOCK < v_hi; v += F32_UNROLL * MC_BLOCK) {
       mc_u32x4 x[F32_UNROLL];
 #pragma unroll
-      for (int j = 0; j < F32_UNROLL; ++j) x[j] = f32_ld<AL>(s + (v + j * MC_BLOCK) * 16);
+      for (int j = 0; j < F32_UNROLL; ++j) x[j] = f32_ld<AL, NT>(s + (v + j * MC_BLOCK) * 16);
 #pragma unroll
       for (int j = 0; j < F32_UNROLL; ++j) {
         if constexpr (COPY) f32_st<AL>(d + (v + j * MC_BLOCK) * 16, x[j]);
@@ -322,10 +322,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_unshuffle(
   }
 }
 
-// slices per chunk for the standalone checksum: ~64 KiB of payload per block,
+// slices per chunk for the standalone checksum: ~32 KiB of payload per block,
 // at least one block per chunk
+static size_t f32_slice_bytes();
+
 static unsigned slices_for(size_t nbytes, size_t nchunks) {
-  size_t sl = nbytes / (64 * 1024);
+  size_t sl = nbytes / f32_slice_bytes();
   if (sl < 1) sl = 1;
   if (sl > 65536) sl = 65536;
   // keep the grid within a 32-bit block count
@@ -338,13 +340,32 @@ static size_t partials_bytes(size_t nchunks, unsigned nslices) {
   return nchunks * (size_t)nslices * 3 * sizeof(uint32_t);
 }
 
-// MCODEC_F32_UNROLL: vectors in flight per thread in k_f32_partial (1 or 4)
+// knobs (read once): MCODEC_F32_UNROLL = vectors in flight per thread in
+// k_f32_partial (1, 4, 8); MCODEC_F32_NTLD = nontemporal loads (0/1);
+// MCODEC_F32_SLICE_KB = payload bytes per workgroup.  Defaults from the sweep
+// on 64 x 4 MiB rows (profiles/r01/fletcher32_knobs_ab.jsonl): 4 loads in
+// flight and 32 KiB slices take the one-pass decode from 116 to 100 us.
+static int f32_env(const char *name, int def) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : def;
+}
 static int f32_unroll() {
   static const int u = [] {
-    const char *e = getenv("MCODEC_F32_UNROLL");
-    return e && atoi(e) == 1 ? 1 : 4;
+    const int e = f32_env("MCODEC_F32_UNROLL", 4);
+    return e == 1 || e == 8 ? e : 4;
   }();
   return u;
+}
+static bool f32_ntld() {
+  static const bool b = f32_env("MCODEC_F32_NTLD", 1) != 0;
+  return b;
+}
+static size_t f32_slice_bytes() {
+  static const size_t b = [] {
+    const int e = f32_env("MCODEC_F32_SLICE_KB", 32);
+    return (size_t)(e >= 4 && e <= 4096 ? e : 32) * 1024;
+  }();
+  return b;
 }
 
 static int align_class(const void *p, size_t stride, size_t nchunks) {
@@ -361,14 +382,22 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
     al = al < ad ? al : ad;
   }
   const unsigned grid = (unsigned)(nchunks * nsl);
+#define MC_F32_U(CP, AL, U)                                                                   \
+  do {                                                                                         \
+    if (f32_ntld())                                                                            \
+      k_f32_partial<CP, AL, U, true><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,          \
+                                                                dst_stride, nbytes, nsl,       \
+                                                                partials);                     \
+    else                                                                                       \
+      k_f32_partial<CP, AL, U, false><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,         \
+                                                                 dst_stride, nbytes, nsl,      \
+                                                                 partials);                    \
+  } while (0)
 #define MC_F32_LAUNCH(CP, AL)                                                                 \
   do {                                                                                         \
-    if (f32_unroll() == 4)                                                                     \
-      k_f32_partial<CP, AL, 4><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride,    \
-                                                          nbytes, nsl, partials);              \
-    else                                                                                       \
-      k_f32_partial<CP, AL, 1><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst, dst_stride,    \
-                                                          nbytes, nsl, partials);              \
+    if (f32_unroll() == 8) MC_F32_U(CP, AL, 8);                                                \
+    else if (f32_unroll() == 4) MC_F32_U(CP, AL, 4);                                           \
+    else MC_F32_U(CP, AL, 1);                                                                  \
   } while (0)
   if (dst) {
     if (al == 2) MC_F32_LAUNCH(true, 2);
@@ -380,6 +409,7 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
     else MC_F32_LAUNCH(false, 0);
   }
 #undef MC_F32_LAUNCH
+#undef MC_F32_U
 }
 
 // standalone driver: checksum (+ optional copy) of nchunks chunks, then finalize

@@ -1,7 +1,5 @@
-# A/B of the checksum tuning knobs on one box (tools/probe_ck_decode.py)
+# A/B of the Fletcher32 kernel knobs on one box (tools/probe_ck_decode.py)
 set -e
-for rep in 1 2; do
-  for env in "MCODEC_F32_UNROLL=1" "MCODEC_F32_UNROLL=4" "MCODEC_CK_KCOPY=16 MCODEC_CK_GRID_COPY=2048" "MCODEC_CK_KCOPY=8 MCODEC_CK_GRID_COPY=1024" "MCODEC_CK_KCOPY=4 MCODEC_CK_GRID_COPY=100000"; do
-    env $env timeout -k 10 120 python tools/probe_ck_decode.py 2>/dev/null
-  done
+for env in "MCODEC_F32_SLICE_KB=64" "MCODEC_F32_SLICE_KB=32" "MCODEC_F32_SLICE_KB=16" "MCODEC_F32_SLICE_KB=8" "MCODEC_F32_SLICE_KB=16 MCODEC_F32_UNROLL=1" "MCODEC_F32_SLICE_KB=32 MCODEC_F32_UNROLL=8" "MCODEC_F32_SLICE_KB=64" "MCODEC_F32_SLICE_KB=32" "MCODEC_F32_SLICE_KB=16"; do
+  env $env PROBE_ONLY=fletcher32 timeout -k 10 120 python tools/probe_ck_decode.py 2>/dev/null
 done
