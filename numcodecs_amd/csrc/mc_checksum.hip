@@ -115,14 +115,6 @@ MC_DEV const CrcConsts &crc_consts() {
 template <int KIND>
 constexpr uint32_t crc_poly() { return KIND == K_CRC32C ? POLY_CRC32C : POLY_CRC32; }
 
-template <int KIND>
-MC_DEV uint32_t xpow(const uint32_t *tab, uint64_t e) {
-  uint32_t p = GF_ONE;
-  for (int k = 0; e; ++k, e >>= 1)
-    if (e & 1) p = gf_mul(p, tab[k], crc_poly<KIND>());
-  return p;
-}
-
 // acc = raw(acc, v ++ zeros(SHIFT)) with the 16 LDS tables
 MC_DEV uint32_t slice16(const uint32_t *__restrict__ V, uint32_t acc, mc_u32x4 v) {
   const uint32_t d = acc ^ v.x;
@@ -311,11 +303,27 @@ MC_DEV void store_le32(uint8_t *p, uint32_t v) {
   p[3] = (uint8_t)(v >> 24);
 }
 
+// Powers of x the CRC finalize needs, the same for every chunk of a call:
+// computed once on the host (a device thread raising x to a 2^25 power with
+// bit-serial products took ~7 us of serial time per call).
+struct CrcFin {
+  uint32_t xt[32];  // (x^(8 * tile bytes))^(2^k)
+  uint32_t pad;     // x^(-8 * zero padding of the last tile)
+  uint32_t xn;      // x^(8 * chunk bytes)
+};
+
+MC_DEV uint32_t xpow_fin(const uint32_t (&xt)[32], uint64_t e, uint32_t poly) {
+  uint32_t p = GF_ONE;
+  for (int k = 0; e; ++k, e >>= 1)
+    if (e & 1) p = gf_mul(p, xt[k], poly);
+  return p;
+}
+
 // One block per chunk: fold the tile partials into the checksum; write it to
 // out[c] (if out) and/or as a little-endian footer at footer + c*footer_stride.
 template <int KIND, int K>
 __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
-    const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
+    const CrcFin fin, const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
     uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride,
     const uint8_t *__restrict__ stored, size_t stored_stride, uint32_t *__restrict__ stored_out) {
   __shared__ uint64_t red[2][MC_BLOCK / 64];
@@ -350,13 +358,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
     const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
     result = (uint32_t)((b << 16) | a);
   } else {
-    const CrcConsts &C = crc_consts<KIND>();
-    constexpr uint64_t TB = (uint64_t)K * STEP;
-    const uint32_t X = xpow<KIND>(C.x2n, 8 * TB);
     uint32_t acc = 0;
     for (size_t j = lo; j < hi; ++j)
-      acc = gf_mul(acc, X, crc_poly<KIND>()) ^ partials[c * tiles_per_chunk + j];
-    if (hi > lo) acc = gf_mul(acc, xpow<KIND>(C.x2n, 8 * TB * (tiles_per_chunk - hi)), crc_poly<KIND>());
+      acc = gf_mul(acc, fin.xt[0], crc_poly<KIND>()) ^ partials[c * tiles_per_chunk + j];
+    if (hi > lo) acc = gf_mul(acc, xpow_fin(fin.xt, tiles_per_chunk - hi, crc_poly<KIND>()), crc_poly<KIND>());
     acc = wave_xor(acc);
     if (lane == 0) red[0][wave] = acc;
     __syncthreads();
@@ -364,9 +369,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
     uint32_t r = 0;
     for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
     // r covers tiles_per_chunk * TB bytes; the last (TB*tiles - n) are padding
-    r = gf_mul(r, xpow<KIND>(C.x2n_inv, 8 * (TB * tiles_per_chunk - n)), crc_poly<KIND>());
+    r = gf_mul(r, fin.pad, crc_poly<KIND>());
     // crc(D, value) = ~raw(~value, D) = ~(~value * x^(8n) xor raw(0, D))
-    result = ~(gf_mul(~init, xpow<KIND>(C.x2n, 8 * (uint64_t)n), crc_poly<KIND>()) ^ r);
+    result = ~(gf_mul(~init, fin.xn, crc_poly<KIND>()) ^ r);
   }
   if (out) out[c] = result;
   if (footer) store_le32(footer + c * footer_stride, result);
@@ -575,6 +580,40 @@ void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n
   else launch_tiles<KIND, K, true, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
 }
 
+// host: x^(2^k) / x^(-2^k) tables (64 squarings, once per polynomial)
+struct HostPow {
+  uint32_t x2n[64], x2n_inv[64];
+  explicit HostPow(uint32_t poly) {
+    x2n[0] = GF_X;
+    x2n_inv[0] = (poly << 1) | 1u;
+    for (int k = 1; k < 64; ++k) {
+      x2n[k] = gf_mul(x2n[k - 1], x2n[k - 1], poly);
+      x2n_inv[k] = gf_mul(x2n_inv[k - 1], x2n_inv[k - 1], poly);
+    }
+  }
+  static uint32_t pw(const uint32_t (&t)[64], uint64_t e, uint32_t poly) {
+    uint32_t p = GF_ONE;
+    for (int k = 0; e; ++k, e >>= 1)
+      if (e & 1) p = gf_mul(p, t[k], poly);
+    return p;
+  }
+};
+
+template <int KIND>
+CrcFin crc_fin(int K, size_t tpc, size_t n) {
+  CrcFin f{};
+  if constexpr (KIND != K_ADLER) {
+    constexpr uint32_t poly = crc_poly<KIND>();
+    static const HostPow hp(poly);
+    const uint64_t tb = (uint64_t)K * STEP;
+    f.xt[0] = HostPow::pw(hp.x2n, 8 * tb, poly);
+    for (int k = 1; k < 32; ++k) f.xt[k] = gf_mul(f.xt[k - 1], f.xt[k - 1], poly);
+    f.pad = HostPow::pw(hp.x2n_inv, 8 * (tb * tpc - n), poly);
+    f.xn = HostPow::pw(hp.x2n, 8 * (uint64_t)n, poly);
+  }
+  return f;
+}
+
 template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
                   uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
@@ -589,7 +628,7 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   case KK:                                                                                     \
     dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, st);                        \
     k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                           \
-        parts, tpc, n, init, out, footer, fs, stored, ss, stored_out);                         \
+        crc_fin<KIND>(KK, tpc, n), parts, tpc, n, init, out, footer, fs, stored, ss, stored_out); \
     break;
     MC_CK_CASE(1)
     MC_CK_CASE(4)
