@@ -20,7 +20,9 @@ Printed (rank 0): ONE JSON line with the contract's keys plus
                   duration, from a HIP event pair on the launch stream
                   bracketing the timed region; peak 8 TB/s; `traffic` = HBM
                   bytes per launch from the rocprofv3 PMC counters committed
-                  under profiles/ (null when absent);
+                  under profiles/ (null when absent); `achievable` = an
+                  on-device 1 GiB DtoD copy measured in the same run (the
+                  practical HBM ceiling of SURVEY §8d) and achieved / it;
   cpu_baseline -- the reference's own Cython _doShuffle/_doUnshuffle
                   (src/numcodecs/_shuffle.pyx, compiled from the reference
                   sources into oracle/_ref by oracle/build_ref.sh) on one host
@@ -456,6 +458,35 @@ def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
     return res
 
 
+def copy_ceiling(dev, nbytes: int = GiB, reps: int = 10):
+    """SURVEY §8d's "achievable" line: on-device DtoD copies of 1 GiB (more
+    than the 256 MiB Infinity Cache) timed in this run -- hipMemcpyAsync (via
+    torch's copy_) and libmcodec's own nontemporal copy kernel (mc_copy);
+    GB/s = read + write bytes / median time of `reps` after a warm-up."""
+    from numcodecs_amd import _ops
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+
+    def rate(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        ts.sort()
+        return round(2 * nbytes / ts[len(ts) // 2] / 1e9, 1)
+
+    res = {"hipMemcpyDtoD_GBps": rate(lambda: b.copy_(a)), "mc_copy_GBps": rate(lambda: _ops.copy(a, b, nbytes))}
+    del a, b
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -503,6 +534,7 @@ def main():
     if rank == 0:
         achieved = 2 * CHUNK / (launch_ms * 1e-3) / 1e9  # GB/s per launch
         traffic, traffic_src = pmc_traffic()
+        ceiling = copy_ceiling(dev)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -533,6 +565,9 @@ def main():
                 "traffic_source": traffic_src,
                 "mean_launch_ms": round(launch_ms, 4),
                 "timing": "HIP events bracketing the timed region on the launch stream / (2 x steps)",
+                "achievable": {"what": "on-device DtoD copies of 1 GiB in this run, read+write bytes / time; "
+                                       "frac = achieved / the faster copy",
+                               **ceiling, "frac": round(achieved / max(ceiling.values()), 4)},
             },
         }
     if rank == 0 and c5:
@@ -551,6 +586,7 @@ def main():
             "frac": round(per_launch / (launch_ms * 1e-3) / 1e9 / PEAK_GBPS, 4),
             "traffic": None, "traffic_source": None,
         })
+        result["roofline"]["achievable"]["frac"] = round(result["roofline"]["achieved"] / max(ceiling.values()), 4)
     if rank == 0 and args.extra:
         result["extra"] = extra_workloads(dev)
     if rank == 0 and args.e2e:

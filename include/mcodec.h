@@ -81,6 +81,16 @@ const char *mc_strerror(int status);
 /* number of HIP devices visible to the runtime the library is bound to */
 int mc_device_count(void);
 
+/* Device-to-device copy (the codecs' pass-through cases: Shuffle with
+ * elementsize <= 1, shuffle.py:31-33; AsType to the same dtype; decode into
+ * `out`, compat.py:173-206 ndarray_copy): nbytes from src to dst, or `rows`
+ * rows of `width` bytes at src + r*src_stride -> dst + r*dst_stride.  src
+ * and dst must not overlap. */
+int mc_copy(const void *src, void *dst, size_t nbytes, mc_stream_t stream);
+int mc_copy_rows(const void *src, size_t src_stride, void *dst,
+                 size_t dst_stride, size_t width, size_t rows,
+                 mc_stream_t stream);
+
 /* ---- Shuffle ---------------------------------------------------------- */
 /* Byte transpose of the (nbytes/elementsize, elementsize) byte matrix:
  *   dst[b*count + i] = src[i*elementsize + b],  count = nbytes/elementsize.

@@ -131,6 +131,8 @@ _SIGNATURES = {
         _c_vp, _c_vp, _c_vp, _c_size, _c_vp,
     ],
     "mc_packbits": [_c_vp, _c_vp, _c_size, _c_vp],
+    "mc_copy": [_c_vp, _c_vp, _c_size, _c_vp],
+    "mc_copy_rows": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp],
     "mc_blosc_filter": [_c_vp, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_unpackbits": [_c_vp, _c_size, _c_vp, _c_size, _c_vp],
 }

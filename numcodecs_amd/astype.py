@@ -26,7 +26,7 @@ def _cast(buf, from_dt, to_dt):
     shape = _view_shape(src.shape, src.dtype.itemsize, from_dt.itemsize, src.order)
     dst = empty_like_bytes(n * to_dt.itemsize, src)
     if from_dt == to_dt:
-        dst.copy_(src.data)
+        _ops.copy(src.data, dst, src.nbytes)
     else:
         _ops.cast(src.data, dst, n, from_dt, to_dt)
     return finish(dst, to_dt, shape, src.order, src.host)

@@ -26,7 +26,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import _native
+from . import _native, _ops
 
 __all__ = [
     "DBuf",
@@ -288,7 +288,10 @@ def ndarray_copy(src, dst):
             raise ValueError(
                 f"cannot copy {s_raw.numel()} bytes into an output buffer of {d_raw.numel()} bytes"
             )
-        d_raw.copy_(s_raw)
+        if s_raw.device == d_raw.device:
+            _ops.copy(s_raw, d_raw, s_raw.numel())
+        else:
+            d_raw.copy_(s_raw)
         return dst
     # host destination
     d = ensure_ndarray_like(dst)

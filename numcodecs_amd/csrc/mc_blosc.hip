@@ -266,7 +266,7 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   if (mode == MC_BLOSC_NOSHUFFLE || (mode == MC_BLOSC_SHUFFLE && typesize == 1))
-    return mc_hip_status(hipMemcpyAsync(d, s, nbytes, hipMemcpyDeviceToDevice, st));
+    return mc_copy_rows_impl(s, nbytes, d, nbytes, nbytes, 1, st);
   if (mode == MC_BLOSC_SHUFFLE) {
     // full blocks as one batch on the Shuffle kernels, then the last block
     const size_t full = nbytes / blocksize, body = blocksize / typesize * typesize;
@@ -276,8 +276,7 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
                    : mc_unshuffle_batch(s, blocksize, d, blocksize, full, body, typesize, stream);
       if (rc != MC_OK) return rc;
       if (body < blocksize)  // trailing bytes of every full block
-        rc = mc_hip_status(hipMemcpy2DAsync(d + body, blocksize, s + body, blocksize,
-                                            blocksize - body, full, hipMemcpyDeviceToDevice, st));
+        rc = mc_copy_rows_impl(s + body, blocksize, d + body, blocksize, blocksize - body, full, st);
       if (rc != MC_OK) return rc;
     }
     const size_t last = nbytes - full * blocksize;
@@ -290,7 +289,7 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
         if (rc != MC_OK) return rc;
       }
       if (lb < last)
-        rc = mc_hip_status(hipMemcpyAsync(ld + lb, ls + lb, last - lb, hipMemcpyDeviceToDevice, st));
+        rc = mc_copy_rows_impl(ls + lb, last - lb, ld + lb, last - lb, last - lb, 1, st);
     }
     return rc;
   }

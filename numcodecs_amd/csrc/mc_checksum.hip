@@ -657,8 +657,8 @@ int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, si
                                     ws, ws_bytes, st);
     case MC_CK_JENKINS: {
       if (d && n) {
-        const hipError_t e = hipMemcpy2DAsync(d, ds, s, ss, n, nchunks, hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return mc_hip_status(e);
+        const int rc = mc_copy_rows_impl(s, ss, d, ds, n, nchunks, st);
+        if (rc != MC_OK) return rc;
       }
       const unsigned grid = (unsigned)((nchunks + 63) / 64);
       k_jenkins<<<grid, 64, 0, st>>>(s, ss, nchunks, n, init, prefix, plen, out, footer, fs, stored,

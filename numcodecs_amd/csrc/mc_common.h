@@ -67,6 +67,11 @@ MC_DEV void mc_st4(void *p, uint32_t v) {
 // launch-error check after a <<<>>> launch
 static inline int mc_last_launch() { return mc_hip_status(hipGetLastError()); }
 
+// rows of `width` bytes, DtoD on `st` (mc_copy.hip): nontemporal 16-B vector
+// kernel for 16-/4-B aligned rows, hipMemcpy(2D)Async otherwise
+int mc_copy_rows_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride, size_t width,
+                      size_t rows, hipStream_t st);
+
 static constexpr int MC_BLOCK = 256;  // 4 waves of 64 lanes
 
 // grid cap for grid-stride streaming kernels: 256 CUs x 8 blocks of 256 threads

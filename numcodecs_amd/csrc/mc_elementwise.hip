@@ -282,8 +282,7 @@ int mc_bitround(const void *src, void *dst, size_t n, int itemsize, int keepbits
   if (!src || !dst) return MC_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const size_t nbytes = n * (size_t)itemsize;
-  if (keepbits == mbits)
-    return mc_hip_status(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToDevice, st));
+  if (keepbits == mbits) return mc_copy_rows_impl(src, nbytes, dst, nbytes, nbytes, 1, st);
   const McBitRound br = mc_make_bitround(itemsize, keepbits);
   const bool vec = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0);
   const size_t per = 16 * STEPS * MC_BLOCK;

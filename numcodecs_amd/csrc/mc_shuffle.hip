@@ -634,10 +634,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   if (nchunks > 1 && (src_stride < chunk_bytes || dst_stride < chunk_bytes)) return MC_EINVAL;
 
   if (es == 1 && br == nullptr) {  // "no shuffling needed" (shuffle.py:31-33)
-    if (nchunks == 1)
-      return mc_hip_status(hipMemcpyAsync(dst, src, chunk_bytes, hipMemcpyDeviceToDevice, st));
-    return mc_hip_status(hipMemcpy2DAsync(dst, dst_stride, src, src_stride, chunk_bytes,
-                                          nchunks, hipMemcpyDeviceToDevice, st));
+    return mc_copy_rows_impl(src, src_stride, dst, dst_stride, chunk_bytes, nchunks, st);
   }
 
   ChunkMap m;

@@ -69,7 +69,7 @@ class Fletcher32(Codec):
             if is_device_tensor(out):
                 out_flat = ensure_contiguous_ndarray(out)
                 out_raw = out_flat.view(torch.uint8) if out_flat.numel() else out_flat.new_empty(0, dtype=torch.uint8)
-                out_raw[: payload.numel()].copy_(payload)
+                _ops.copy(payload, out_raw, payload.numel())
                 return out
             o = ensure_contiguous_ndarray(out).view("uint8")
             o[: payload.numel()] = download(payload)

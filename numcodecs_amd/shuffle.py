@@ -55,7 +55,7 @@ class Shuffle(Codec):
             else:
                 res = empty_like_bytes(nbytes, src)
         if es <= 1:  # no shuffling needed (shuffle.py:31-33)
-            res[:nbytes].copy_(src.data)
+            _ops.copy(src.data, res, nbytes)
         else:
             _ops.shuffle(src.data, res, nbytes, es, encode)
         if host_out is not None:
