@@ -125,6 +125,21 @@ def test_jenkins_sizes_device(device):
         assert jenkins_lookup3(y) == oracle.jenkins_lookup3(x)
 
 
+def test_jenkins_sizes_and_batches(device):
+    """The Jenkins kernel around its 192-B prefetch groups and every tail
+    length, single chunks and batches of many small rows."""
+    for n in (0, 1, 12, 13, 767, 768, 769, 780, 781, 768 * 8 - 1, 768 * 8 + 11, 768 * 9 + 5, 768 * 17 + 12,
+              (1 << 20) + 7):
+        x = RNG.integers(0, 256, n, dtype=np.uint8)
+        xd = torch.from_numpy(x).to(device)
+        assert jenkins_lookup3(xd, 77) == oracle.jenkins_lookup3(x, 77), n
+    for b, n in ((2100, 100), (2048, 37), (7, 768 * 3 + 4)):
+        rows = torch.randint(0, 256, (b, n), dtype=torch.uint8, device=device)
+        host = rows.cpu().numpy()
+        sums = batch.checksum32_chunks(rows, "jenkins_lookup3", value=5)
+        assert sums.tolist() == [oracle.jenkins_lookup3(host[i], 5) for i in range(b)], (b, n)
+
+
 @pytest.mark.parametrize("codec_id", ["crc32", "crc32c", "adler32", "jenkins_lookup3"])
 def test_checksum_batches(device, codec_id):
     ref = {**REF, "jenkins_lookup3": oracle.jenkins_lookup3}[codec_id]
