@@ -411,6 +411,8 @@ static void launch_int_scan(const uint8_t *s, uint8_t *d, size_t n, int a, int d
 // ---------------------------------------------------------------------------
 constexpr int DS_GROUP = 4;
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
 template <int ES>
 using dacc_t = typename std::conditional<ES == 8, uint64_t, uint32_t>::type;
 
@@ -438,6 +440,27 @@ MC_DEV void ds_load(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v)[ds_
   } else {
 #pragma unroll
     for (int i = 0; i < PER; ++i) v[i] = e0 + i < n ? (dacc_t<ES>)mc_load_elem(src, e0 + i, ES) : 0;
+  }
+}
+
+// the values of elements [e0, e0 + PER/2) (one 16-B vector; zeros past n)
+// into v[at .. at + PER/2)
+template <int ES>
+MC_DEV void ds_load_half(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v)[ds_per<ES>()], int at) {
+  constexpr int H = ds_per<ES>() / 2;
+  if (e0 + H <= n) {
+    const mc_u32x4 w = mc_ld16<true>(src + e0 * ES);
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      if constexpr (ES == 1) v[at + i] = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      else if constexpr (ES == 2) v[at + i] = (d[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      else if constexpr (ES == 4) v[at + i] = d[i];
+      else v[at + i] = ((uint64_t)d[2 * i + 1] << 32) | d[2 * i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < H; ++i) v[at + i] = e0 + i < n ? (dacc_t<ES>)mc_load_elem(src, e0 + i, ES) : 0;
   }
 }
 
@@ -469,15 +492,51 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce(const uint8_t *__rest
   __shared__ uint64_t lds[DS_GROUP][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t t0 = (size_t)blockIdx.x * DS_GROUP;  // first tile of the group
-  dacc_t<ES> v[DS_GROUP][PER];
-#pragma unroll
-  for (int h = 0; h < DS_GROUP; ++h) ds_load<ES>(src, n, (t0 + h) * TE + (size_t)threadIdx.x * PER, v[h]);
+  // a tile total does not depend on which thread adds which element, so the
+  // loads are lane-contiguous 16-B vectors (each wave instruction covers 1 KiB
+  // contiguously) instead of the apply pass's 32 B per thread: half of tile h
+  // at 16*tid and the other half 16*MC_BLOCK bytes later.  Totals are only
+  // needed mod 2^(8*ES), so bytes and halfwords are summed per dword with
+  // v_dot4_u32_u8 / v_dot2_u32_u16 instead of one extract + add per element.
   uint64_t acc[DS_GROUP];
+  if ((t0 + DS_GROUP) * TE <= n) {
 #pragma unroll
-  for (int h = 0; h < DS_GROUP; ++h) {
-    acc[h] = 0;
+    for (int h = 0; h < DS_GROUP; ++h) {
+      const uint8_t *tb = src + (t0 + h) * TE * ES;
+      const mc_u32x4 w0 = mc_ld16<true>(tb + 16 * (size_t)threadIdx.x);
+      const mc_u32x4 w1 = mc_ld16<true>(tb + 16 * (size_t)(MC_BLOCK + threadIdx.x));
+      const uint32_t d[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      if constexpr (ES == 8) {
+        uint64_t a = 0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) acc[h] += v[h][i];
+        for (int i = 0; i < 4; ++i) a += ((uint64_t)d[2 * i + 1] << 32) | d[2 * i];
+        acc[h] = a;
+      } else {
+        uint32_t a = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if constexpr (ES == 1) a = __builtin_amdgcn_udot4(d[i], 0x01010101u, a, false);
+          else if constexpr (ES == 2) a = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[i]), ushort2_t{1, 1}, a, false);
+          else a += d[i];
+        }
+        acc[h] = a;
+      }
+    }
+  } else {
+    constexpr int HALF = PER / 2;
+    dacc_t<ES> v[DS_GROUP][PER];
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) {
+      const size_t tb = (t0 + h) * TE;
+      ds_load_half<ES>(src, n, tb + (size_t)threadIdx.x * HALF, v[h], 0);
+      ds_load_half<ES>(src, n, tb + (size_t)(MC_BLOCK + threadIdx.x) * HALF, v[h], HALF);
+    }
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) {
+      acc[h] = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) acc[h] += v[h][i];
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1)
@@ -500,29 +559,100 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce(const uint8_t *__rest
   }
 }
 
+// elements [e0, e0 + PER/2) from v[at ..] (one 16-B vector; nothing past n)
+template <int ES>
+MC_DEV void ds_store_half(uint8_t *dst, size_t n, size_t e0, const dacc_t<ES> (&v)[ds_per<ES>()], int at) {
+  constexpr int H = ds_per<ES>() / 2;
+  if (e0 + H <= n) {
+    uint32_t d[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      if constexpr (ES == 1) d[i >> 2] |= ((uint32_t)v[at + i] & 0xffu) << (8 * (i & 3));
+      else if constexpr (ES == 2) d[i >> 1] |= ((uint32_t)v[at + i] & 0xffffu) << (16 * (i & 1));
+      else if constexpr (ES == 4) d[i] = (uint32_t)v[at + i];
+      else { d[2 * i] = (uint32_t)v[at + i]; d[2 * i + 1] = (uint32_t)((uint64_t)v[at + i] >> 32); }
+    }
+    mc_st16<true>(dst + e0 * ES, mc_u32x4{d[0], d[1], d[2], d[3]});
+  } else {
+    for (int i = 0; i < H && e0 + i < n; ++i) mc_store_elem(dst, e0 + i, ES, (uint64_t)v[at + i]);
+  }
+}
+
+// exclusive block scans of two per-thread values at once (the two halves of
+// a tile), modulo 2^(8 * sizeof(T)), one LDS round; *tot_a = block total of a
+template <typename T>
+MC_DEV void ds_block_scan2(T a, T b, T (&lds)[2][MC_BLOCK / 64], T &ea, T &eb, T &tot_a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T ia = a, ib = b;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T oa = __shfl_up(ia, off, 64), ob = __shfl_up(ib, off, 64);
+    if (lane >= off) {
+      ia += oa;
+      ib += ob;
+    }
+  }
+  if (lane == 63) {
+    lds[0][wave] = ia;
+    lds[1][wave] = ib;
+  }
+  __syncthreads();
+  T pa = 0, pb = 0, ta = 0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) {
+    const T xa = lds[0][w], xb = lds[1][w];
+    if (w < wave) {
+      pa += xa;
+      pb += xb;
+    }
+    ta += xa;
+  }
+  const T ua = __shfl_up(ia, 1, 64), ub = __shfl_up(ib, 1, 64);
+  ea = pa + (lane ? ua : (T)0);
+  eb = pb + (lane ? ub : (T)0);
+  tot_a = ta;
+}
+
+// Scan of one tile with lane-contiguous 16-B accesses: thread t owns the
+// vector at 16*t of each half of the tile (half A = the first 16*MC_BLOCK
+// bytes, half B = the rest), scans both in registers, and one two-value
+// block scan gives every vector its prefix (B's offset by A's total).  Each
+// wave load/store instruction covers 1 KiB contiguously (the 32-B-per-thread
+// layout touched 2 KiB with gaps per instruction).
 template <int ES>
 __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply(const uint8_t *__restrict__ src,
                                                          uint8_t *__restrict__ dst, size_t n,
                                                          const uint64_t *__restrict__ group_pre,
                                                          const uint64_t *__restrict__ part) {
   constexpr int PER = ds_per<ES>();
-  __shared__ uint64_t lds[MC_BLOCK / 64];
+  constexpr int H = PER / 2;
+  using T = dacc_t<ES>;
+  __shared__ T lds[2][MC_BLOCK / 64];
   const size_t tile = blockIdx.x;
-  const size_t e0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * PER;
-  dacc_t<ES> v[PER];
-  ds_load<ES>(src, n, e0, v);
-  dacc_t<ES> run = 0;
+  const size_t ea0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * H;
+  const size_t eb0 = tile * ds_tile<ES>() + (size_t)(MC_BLOCK + threadIdx.x) * H;
+  T v[PER];
+  ds_load_half<ES>(src, n, ea0, v, 0);
+  ds_load_half<ES>(src, n, eb0, v, H);
+  T ra = 0, rb = 0;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    run += v[i];
-    v[i] = run;
+  for (int i = 0; i < H; ++i) {
+    ra += v[i];
+    v[i] = ra;
+    rb += v[H + i];
+    v[H + i] = rb;
   }
-  uint64_t tot;
-  const uint64_t excl = mc_block_excl_scan<false>((uint64_t)run, lds, &tot);
-  const dacc_t<ES> pre = (dacc_t<ES>)(group_pre[tile / DS_GROUP] + part[tile] + excl);
+  T xa, xb, ta;
+  ds_block_scan2<T>(ra, rb, lds, xa, xb, ta);
+  const T pre = (T)(group_pre[tile / DS_GROUP] + part[tile]);
+  const T pa = pre + xa, pb = pre + ta + xb;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) v[i] += pre;
-  ds_store<ES>(dst, n, e0, v);
+  for (int i = 0; i < H; ++i) {
+    v[i] += pa;
+    v[H + i] += pb;
+  }
+  ds_store_half<ES>(dst, n, ea0, v, 0);
+  ds_store_half<ES>(dst, n, eb0, v, H);
 }
 
 // workspace entries of the fast path: part[] (whole groups of tiles) + group sums
