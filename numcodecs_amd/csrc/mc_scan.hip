@@ -421,28 +421,6 @@ constexpr int ds_per() { return 32 / ES; }
 template <int ES>
 constexpr size_t ds_tile() { return (size_t)ds_per<ES>() * MC_BLOCK; }
 
-// the values of elements [e0, e0 + PER) (zeros past n)
-template <int ES>
-MC_DEV void ds_load(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v)[ds_per<ES>()]) {
-  constexpr int PER = ds_per<ES>();
-  if (e0 + PER <= n) {
-    mc_u32x4 w[2];
-    w[0] = mc_ld16<true>(src + e0 * ES);
-    w[1] = mc_ld16<true>(src + e0 * ES + 16);
-    const uint32_t *d = reinterpret_cast<const uint32_t *>(w);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if constexpr (ES == 1) v[i] = (d[i >> 2] >> (8 * (i & 3))) & 0xffu;
-      else if constexpr (ES == 2) v[i] = (d[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      else if constexpr (ES == 4) v[i] = d[i];
-      else v[i] = ((uint64_t)d[2 * i + 1] << 32) | d[2 * i];
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = e0 + i < n ? (dacc_t<ES>)mc_load_elem(src, e0 + i, ES) : 0;
-  }
-}
-
 // the values of elements [e0, e0 + PER/2) (one 16-B vector; zeros past n)
 // into v[at .. at + PER/2)
 template <int ES>
@@ -464,24 +442,6 @@ MC_DEV void ds_load_half(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v
   }
 }
 
-template <int ES>
-MC_DEV void ds_store(uint8_t *dst, size_t n, size_t e0, const dacc_t<ES> (&v)[ds_per<ES>()]) {
-  constexpr int PER = ds_per<ES>();
-  if (e0 + PER <= n) {
-    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if constexpr (ES == 1) d[i >> 2] |= ((uint32_t)v[i] & 0xffu) << (8 * (i & 3));
-      else if constexpr (ES == 2) d[i >> 1] |= ((uint32_t)v[i] & 0xffffu) << (16 * (i & 1));
-      else if constexpr (ES == 4) d[i] = (uint32_t)v[i];
-      else { d[2 * i] = (uint32_t)v[i]; d[2 * i + 1] = (uint32_t)((uint64_t)v[i] >> 32); }
-    }
-    mc_st16<true>(dst + e0 * ES, mc_u32x4{d[0], d[1], d[2], d[3]});
-    mc_st16<true>(dst + e0 * ES + 16, mc_u32x4{d[4], d[5], d[6], d[7]});
-  } else {
-    for (int i = 0; i < PER && e0 + i < n; ++i) mc_store_elem(dst, e0 + i, ES, (uint64_t)v[i]);
-  }
-}
 
 template <int ES>
 __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce(const uint8_t *__restrict__ src, size_t n,
@@ -579,9 +539,10 @@ MC_DEV void ds_store_half(uint8_t *dst, size_t n, size_t e0, const dacc_t<ES> (&
 }
 
 // exclusive block scans of two per-thread values at once (the two halves of
-// a tile), modulo 2^(8 * sizeof(T)), one LDS round; *tot_a = block total of a
+// a tile), modulo 2^(8 * sizeof(T)), one LDS round (one __syncthreads; a
+// caller that loops alternates two `lds` buffers); tot_a / tot_b = totals
 template <typename T>
-MC_DEV void ds_block_scan2(T a, T b, T (&lds)[2][MC_BLOCK / 64], T &ea, T &eb, T &tot_a) {
+MC_DEV void ds_block_scan2(T a, T b, T (&lds)[2][MC_BLOCK / 64], T &ea, T &eb, T &tot_a, T &tot_b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   T ia = a, ib = b;
 #pragma unroll
@@ -597,7 +558,7 @@ MC_DEV void ds_block_scan2(T a, T b, T (&lds)[2][MC_BLOCK / 64], T &ea, T &eb, T
     lds[1][wave] = ib;
   }
   __syncthreads();
-  T pa = 0, pb = 0, ta = 0;
+  T pa = 0, pb = 0, ta = 0, tb = 0;
 #pragma unroll
   for (int w = 0; w < MC_BLOCK / 64; ++w) {
     const T xa = lds[0][w], xb = lds[1][w];
@@ -606,11 +567,13 @@ MC_DEV void ds_block_scan2(T a, T b, T (&lds)[2][MC_BLOCK / 64], T &ea, T &eb, T
       pb += xb;
     }
     ta += xa;
+    tb += xb;
   }
   const T ua = __shfl_up(ia, 1, 64), ub = __shfl_up(ib, 1, 64);
   ea = pa + (lane ? ua : (T)0);
   eb = pb + (lane ? ub : (T)0);
   tot_a = ta;
+  tot_b = tb;
 }
 
 // Scan of one tile with lane-contiguous 16-B accesses: thread t owns the
@@ -642,8 +605,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply(const uint8_t *__restr
     rb += v[H + i];
     v[H + i] = rb;
   }
-  T xa, xb, ta;
-  ds_block_scan2<T>(ra, rb, lds, xa, xb, ta);
+  T xa, xb, ta, tb;
+  ds_block_scan2<T>(ra, rb, lds, xa, xb, ta, tb);
   const T pre = (T)(group_pre[tile / DS_GROUP] + part[tile]);
   const T pa = pre + xa, pb = pre + ta + xb;
 #pragma unroll
@@ -663,38 +626,53 @@ static size_t dscan_ws_entries(size_t n, int es) {
 }
 
 // Batched same-width integer Delta decode: one workgroup per chunk walks it in
-// 8 KiB tiles (32 B per thread, one block scan per tile) with a running
-// carry; the next tile's loads are issued before the current tile's scan.
+// 8 KiB tiles with a running carry, the next tile's loads issued before the
+// current tile's scan; the two-half tile layout of k_dscan_apply.
 template <int ES>
 __global__ __launch_bounds__(MC_BLOCK) void k_dscan_rows(const uint8_t *__restrict__ src,
                                                         size_t src_stride,
                                                         uint8_t *__restrict__ dst,
                                                         size_t dst_stride, size_t n) {
   constexpr int PER = ds_per<ES>();
+  constexpr int H = PER / 2;
   constexpr size_t TE = ds_tile<ES>();
-  __shared__ uint64_t lds[MC_BLOCK / 64];
+  using T = dacc_t<ES>;
+  __shared__ T lds[2][2][MC_BLOCK / 64];  // [iteration parity][half][wave]
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
-  dacc_t<ES> carry = 0;
-  dacc_t<ES> nxt[PER];
-  ds_load<ES>(src, n, (size_t)threadIdx.x * PER, nxt);
-  for (size_t base = 0; base < n; base += TE) {
-    dacc_t<ES> v[PER];
+  const size_t oa = (size_t)threadIdx.x * H, ob = (size_t)(MC_BLOCK + threadIdx.x) * H;
+  T carry = 0;
+  T nxt[PER];
+  ds_load_half<ES>(src, n, oa, nxt, 0);
+  ds_load_half<ES>(src, n, ob, nxt, H);
+  int parity = 0;
+  for (size_t base = 0; base < n; base += TE, parity ^= 1) {
+    T v[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) v[i] = nxt[i];
-    if (base + TE < n) ds_load<ES>(src, n, base + TE + (size_t)threadIdx.x * PER, nxt);
-    dacc_t<ES> run = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      run += v[i];
-      v[i] = run;
+    if (base + TE < n) {
+      ds_load_half<ES>(src, n, base + TE + oa, nxt, 0);
+      ds_load_half<ES>(src, n, base + TE + ob, nxt, H);
     }
-    uint64_t tot;
-    const dacc_t<ES> pre = carry + (dacc_t<ES>)mc_block_excl_scan<false>((uint64_t)run, lds, &tot);
+    T ra = 0, rb = 0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] += pre;
-    ds_store<ES>(dst, n, base + (size_t)threadIdx.x * PER, v);
-    carry += (dacc_t<ES>)tot;
+    for (int i = 0; i < H; ++i) {
+      ra += v[i];
+      v[i] = ra;
+      rb += v[H + i];
+      v[H + i] = rb;
+    }
+    T xa, xb, ta, tb;
+    ds_block_scan2<T>(ra, rb, lds[parity], xa, xb, ta, tb);
+    const T pa = carry + xa, pb = carry + ta + xb;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      v[i] += pa;
+      v[H + i] += pb;
+    }
+    ds_store_half<ES>(dst, n, base + oa, v, 0);
+    ds_store_half<ES>(dst, n, base + ob, v, H);
+    carry += ta + tb;
   }
 }
 
