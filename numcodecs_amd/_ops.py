@@ -212,8 +212,7 @@ def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
         pair = torch.empty(2, dtype=torch.int32, device=src.device)
         check(lib.mc_fletcher32_verify(src.data_ptr(), nbytes, pair.data_ptr(), ws.data_ptr(),
                                        ws.numel(), stream(src)), "mc_fletcher32_verify")
-        v = pair.cpu().numpy().view(np.uint32)
-    return int(v[0]), int(v[1])
+        return _read_pair(pair)
 
 
 def fletcher32(src, nbytes) -> int:
@@ -286,6 +285,33 @@ def checksum32_decode(kind, src, src_stride, dst, dst_stride, nchunks, encoded_b
                                              stream(src)),
               "mc_checksum32_decode_batch")
     return sums[:nchunks], stored[:nchunks]
+
+
+def _read_pair(dev: torch.Tensor) -> "tuple[int, int]":
+    """Two device uint32 words -> host ints: one async copy into pinned
+    memory and a stream sync (no pageable hipMemcpy)."""
+    host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    host.copy_(dev, non_blocking=True)
+    torch.cuda.current_stream(dev.device).synchronize()
+    v = host.numpy().view(np.uint32)
+    return int(v[0]), int(v[1])
+
+
+def checksum32_verify(kind, src, encoded_bytes, init, location, prefix=None) -> "tuple[int, int]":
+    """(computed, stored) checksum of ONE encoded buffer (payload + 4 bytes
+    at `location`), from one mc_checksum32_decode_batch call (syncs)."""
+    _native.require_device()
+    pair = torch.empty(2, dtype=torch.int32, device=src.device)
+    with _guard(src):
+        pre = _prefix_dev(prefix, src)
+        ws = workspace(lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4), src)
+        check(lib.mc_checksum32_decode_batch(kind, src.data_ptr(), encoded_bytes, None, 0, 1, encoded_bytes,
+                                             init & 0xFFFFFFFF, pre.data_ptr() if pre is not None else None,
+                                             pre.numel() if pre is not None else 0, location,
+                                             pair.data_ptr(), pair.data_ptr() + 4, ws.data_ptr(), ws.numel(),
+                                             stream(src)),
+              "mc_checksum32_decode_batch")
+        return _read_pair(pair)
 
 
 def packbits(src, dst, n) -> None:

@@ -85,13 +85,8 @@ class Checksum32(Codec):
         n = src.nbytes
         if n < 4:
             raise ValueError("Input buffer is too short to contain a 32-bit checksum.")
-        if self.location == "start":
-            stored, payload = src.data[:4], src.data[4:]
-        else:
-            stored, payload = src.data[n - 4:], src.data[: n - 4]
-        computed = _ops.checksum32(self._kind, payload, n - 4, 1, n - 4, self._value)
-        pair = download(torch.cat([_raw(computed), stored])).view("<u4")
-        checksum, expect = int(pair[0]), pair[1]
+        payload = src.data[4:] if self.location == "start" else src.data[: n - 4]
+        checksum, expect = _ops.checksum32_verify(self._kind, src.data, n, self._value, self._loc())
         if expect != checksum:
             raise RuntimeError(
                 f"Stored and computed {self.codec_id} checksum do not match. "
@@ -216,9 +211,8 @@ class JenkinsLookup3(Checksum32):
         n = src.nbytes
         if n < 4:  # b[-4:].view('<u4') of fewer than 4 bytes fails in numpy
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
-        val_t = self._hash(src.data[: n - 4], n - 4)
-        pair = download(torch.cat([_raw(val_t), src.data[n - 4:]])).view("<u4")
-        val, found = int(pair[0]), pair[1]
+        val, found = _ops.checksum32_verify(_native.MC_CK_JENKINS, src.data, n, self.initval, _native.MC_CK_END,
+                                            self.prefix)
         if val != found:
             raise RuntimeError(
                 f"The Bob Jenkin's lookup3 checksum of the data ({val}) did not"

@@ -307,17 +307,11 @@ MC_DEV void store_le32(uint8_t *p, uint32_t v) {
 // computed once on the host (a device thread raising x to a 2^25 power with
 // bit-serial products took ~7 us of serial time per call).
 struct CrcFin {
-  uint32_t xt[32];  // (x^(8 * tile bytes))^(2^k)
-  uint32_t pad;     // x^(-8 * zero padding of the last tile)
-  uint32_t xn;      // x^(8 * chunk bytes)
+  uint32_t xb[32];          // X * (bit m): basis of the product by X = x^(8 * tile bytes)
+  uint32_t tail[MC_BLOCK];  // X^(tiles - hi(t)): moves thread t's fold to the chunk end
+  uint32_t pad;             // x^(-8 * zero padding of the last tile)
+  uint32_t xn;              // x^(8 * chunk bytes)
 };
-
-MC_DEV uint32_t xpow_fin(const uint32_t (&xt)[32], uint64_t e, uint32_t poly) {
-  uint32_t p = GF_ONE;
-  for (int k = 0; e; ++k, e >>= 1)
-    if (e & 1) p = gf_mul(p, xt[k], poly);
-  return p;
-}
 
 // One block per chunk: fold the tile partials into the checksum; write it to
 // out[c] (if out) and/or as a little-endian footer at footer + c*footer_stride.
@@ -358,10 +352,24 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
     const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
     result = (uint32_t)((b << 16) | a);
   } else {
+    // Horner over this thread's tiles; the product by the constant X is
+    // linear in the bits of acc: 4 byte tables in LDS built from X's basis
+    __shared__ uint32_t T[4][256];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((threadIdx.x >> k) & 1) r ^= fin.xb[8 * j + k];
+      T[j][threadIdx.x] = r;
+    }
+    __syncthreads();
     uint32_t acc = 0;
+#pragma unroll 4
     for (size_t j = lo; j < hi; ++j)
-      acc = gf_mul(acc, fin.xt[0], crc_poly<KIND>()) ^ partials[c * tiles_per_chunk + j];
-    if (hi > lo) acc = gf_mul(acc, xpow_fin(fin.xt, tiles_per_chunk - hi, crc_poly<KIND>()), crc_poly<KIND>());
+      acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
+            partials[c * tiles_per_chunk + j];
+    if (hi > lo) acc = gf_mul(acc, fin.tail[threadIdx.x], crc_poly<KIND>());
     acc = wave_xor(acc);
     if (lane == 0) red[0][wave] = acc;
     __syncthreads();
@@ -600,18 +608,53 @@ struct HostPow {
 };
 
 template <int KIND>
-CrcFin crc_fin(int K, size_t tpc, size_t n) {
+CrcFin crc_fin_build(int K, size_t tpc, size_t n) {
   CrcFin f{};
   if constexpr (KIND != K_ADLER) {
     constexpr uint32_t poly = crc_poly<KIND>();
     static const HostPow hp(poly);
     const uint64_t tb = (uint64_t)K * STEP;
-    f.xt[0] = HostPow::pw(hp.x2n, 8 * tb, poly);
-    for (int k = 1; k < 32; ++k) f.xt[k] = gf_mul(f.xt[k - 1], f.xt[k - 1], poly);
+    uint32_t xt[32];  // X^(2^k)
+    xt[0] = HostPow::pw(hp.x2n, 8 * tb, poly);
+    for (int k = 1; k < 32; ++k) xt[k] = gf_mul(xt[k - 1], xt[k - 1], poly);
+    for (int m = 0; m < 32; ++m) f.xb[m] = gf_mul(1u << m, xt[0], poly);
+    // tail[t] = X^(tpc - hi(t)), walking t down: each step multiplies by
+    // X^(hi(t+1) - hi(t)), one of two exponents (floor / ceil of tpc/256)
+    const uint64_t d0 = tpc / MC_BLOCK;
+    auto xpow = [&](uint64_t e) {
+      uint32_t p = GF_ONE;
+      for (int k = 0; e; ++k, e >>= 1)
+        if (e & 1) p = gf_mul(p, xt[k], poly);
+      return p;
+    };
+    const uint32_t m0 = xpow(d0), m1 = xpow(d0 + 1);
+    f.tail[MC_BLOCK - 1] = GF_ONE;
+    for (int t = MC_BLOCK - 2; t >= 0; --t) {
+      const uint64_t step = tpc * (t + 2) / MC_BLOCK - tpc * (t + 1) / MC_BLOCK;
+      f.tail[t] = step == 0 ? f.tail[t + 1] : gf_mul(f.tail[t + 1], step == d0 ? m0 : m1, poly);
+    }
     f.pad = HostPow::pw(hp.x2n_inv, 8 * (tb * tpc - n), poly);
     f.xn = HostPow::pw(hp.x2n, 8 * (uint64_t)n, poly);
   }
   return f;
+}
+
+// the constants of the last call on this thread (a stream of equal-size
+// chunks asks for the same ones every time)
+template <int KIND>
+const CrcFin &crc_fin(int K, size_t tpc, size_t n) {
+  thread_local struct {
+    int K = -1;
+    size_t tpc = 0, n = 0;
+    CrcFin f;
+  } last;
+  if (KIND != K_ADLER && (last.K != K || last.tpc != tpc || last.n != n)) {
+    last.f = crc_fin_build<KIND>(K, tpc, n);
+    last.K = K;
+    last.tpc = tpc;
+    last.n = n;
+  }
+  return last.f;
 }
 
 template <int KIND>

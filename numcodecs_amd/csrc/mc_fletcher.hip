@@ -210,6 +210,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
   const size_t c = blockIdx.x;
   F32Part p;
   part_init(p);
+#pragma unroll 8
   for (unsigned sl = threadIdx.x; sl < nslices; sl += MC_BLOCK) {
     const uint32_t *q = partials + 3 * (c * nslices + sl);
     p.s1 += q[0];
