@@ -443,14 +443,18 @@ def end_to_end(dev, total_gib: int = 2, chunk_bytes: int = 4 * MiB):
     codecs = [BitRound(10), Shuffle(4), CRC32()]
     x32 = hin.view(torch.float32)
     x32.copy_(torch.randn(x32.shape))
-    chunks.host_encode_chunks(codecs, x32, henc_z := torch.empty((nchunks, chunk_bytes + 4), dtype=torch.uint8).pin_memory())
-    t0 = time.perf_counter()
-    chunks.host_encode_chunks(codecs, x32, henc_z)
-    te = time.perf_counter() - t0
+    henc_z = torch.empty((nchunks, chunk_bytes + 4), dtype=torch.uint8).pin_memory()
     out = hdec.view(torch.float32)
-    t0 = time.perf_counter()
+    chunks.host_encode_chunks(codecs, x32, henc_z)  # warm-up: allocator pools, lazy init
     chunks.host_decode_chunks(codecs, henc_z, out)
-    td = time.perf_counter() - t0
+    te = td = float("inf")
+    for _ in range(3):  # best of 3 (host-side timing of a PCIe-bound stream)
+        t0 = time.perf_counter()
+        chunks.host_encode_chunks(codecs, x32, henc_z)
+        te = min(te, time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        chunks.host_decode_chunks(codecs, henc_z, out)
+        td = min(td, time.perf_counter() - t0)
     res["zarr_chain_bitround10_shuffle4_crc32"] = {
         "encode_GiBps": round(nchunks * chunk_bytes / GiB / te, 2),
         "decode_GiBps": round(nchunks * chunk_bytes / GiB / td, 2),
