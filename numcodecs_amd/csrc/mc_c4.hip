@@ -250,13 +250,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict
                                                       const uint64_t *__restrict__ first,
                                                       C4Params p) {
   constexpr int DS = D == MC_F4 ? 4 : 8;
-  __shared__ uint64_t red[MC_BLOCK / 64];
+  __shared__ uint32_t red[MC_BLOCK / 64];
   __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
   const size_t tile = blockIdx.x;
   uint32_t v[C4_PER], run;
   c4_local_scan<D, A>(src, tile, p, v, run);
-  uint64_t agg;
-  const uint32_t excl = (uint32_t)mc_block_excl_scan<false>(run, red, &agg);
+  uint32_t agg;
+  const uint32_t excl = mc_block_excl_scan32(run, red, &agg);
   const uint32_t tile_pre = (uint32_t)pair_pre[tile >> 1] + ((tile & 1) ? (uint32_t)first[tile >> 1] : 0u);
   c4_finish<D, A>(dst, tile, v, tile_pre + excl, outb, p);
 }

@@ -46,6 +46,33 @@ MC_DEV uint64_t mc_block_excl_scan(uint64_t v, uint64_t *lds, uint64_t *total) {
   return mc_scan_combine<OR_OP>(wpre, lane ? excl_in_wave : 0);
 }
 
+// 32-bit exclusive block sum scan (mod 2^32): half the shuffle traffic of the
+// 64-bit mc_block_excl_scan for callers whose totals are 32-bit (the int16 /
+// int32 C4 scan).  Same contract: two __syncthreads(), `lds` holds
+// blockDim.x/64 words.
+MC_DEV uint32_t mc_block_excl_scan32(uint32_t v, uint32_t *lds, uint32_t *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwaves = (blockDim.x + 63) >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) lds[wave] = incl;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+  for (int w = 0; w < nwaves; ++w) {
+    const uint32_t x = lds[w];
+    if (w < wave) wpre += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  const uint32_t excl_in_wave = __shfl_up(incl, 1, 64);
+  return wpre + (lane ? excl_in_wave : 0u);
+}
+
 // Exclusive scan of `ntiles` tile totals in place, one workgroup of 1024
 // (tools/scan_bench.hip measures it alone).  Per round of 8192 totals each
 // wave moves its 512 through an LDS slice with coalesced global accesses
