@@ -217,6 +217,93 @@ __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc(const uint8_t *__restric
   }
 }
 
+// Same-width integer Delta encode on 16-B vectors (astype == dtype, 16-B
+// aligned rows).  Wrapping differences are bit operations on the packed
+// vector: the "previous element" vector is the vector shifted up by one
+// element (v_alignbit with the dword before it, which comes from the lane
+// below by a shuffle, or from memory for lane 0 of a wave), and the packed
+// subtraction is SWAR for bytes and halfwords.  Lane-contiguous accesses,
+// DE_V vectors per thread with every load issued first.
+constexpr int DE_V = 4;
+
+template <int ES>
+MC_DEV uint32_t swar_sub(uint32_t a, uint32_t b) {
+  if constexpr (ES == 1) {
+    constexpr uint32_t H = 0x80808080u;
+    return ((a | H) - (b & ~H)) ^ ((a ^ ~b) & H);
+  } else if constexpr (ES == 2) {
+    constexpr uint32_t H = 0x80008000u;
+    return ((a | H) - (b & ~H)) ^ ((a ^ ~b) & H);
+  } else {
+    return a - b;
+  }
+}
+
+template <int ES>
+MC_DEV mc_u32x4 delta_vec(mc_u32x4 x, uint32_t p_lo, uint32_t p_hi) {
+  // p_hi:p_lo = the 8 bytes just before x (p_hi the dword right before x.x)
+  if constexpr (ES == 8) {
+    const uint64_t a0 = ((uint64_t)x.y << 32) | x.x, a1 = ((uint64_t)x.w << 32) | x.z;
+    const uint64_t b0 = ((uint64_t)p_hi << 32) | p_lo;
+    const uint64_t r0 = a0 - b0, r1 = a1 - a0;
+    return mc_u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+  } else if constexpr (ES == 4) {
+    return mc_u32x4{x.x - p_hi, x.y - x.x, x.z - x.y, x.w - x.z};
+  } else {
+    constexpr uint32_t SH = 32 - 8 * ES;  // ({hi, lo} >> SH) = hi << 8ES | lo's top ES bytes
+    const uint32_t s0 = __builtin_amdgcn_alignbit(x.x, p_hi, SH);
+    const uint32_t s1 = __builtin_amdgcn_alignbit(x.y, x.x, SH);
+    const uint32_t s2 = __builtin_amdgcn_alignbit(x.z, x.y, SH);
+    const uint32_t s3 = __builtin_amdgcn_alignbit(x.w, x.z, SH);
+    return mc_u32x4{swar_sub<ES>(x.x, s0), swar_sub<ES>(x.y, s1), swar_sub<ES>(x.z, s2),
+                    swar_sub<ES>(x.w, s3)};
+  }
+}
+
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__restrict__ src,
+                                                             uint8_t *__restrict__ dst, size_t nbytes,
+                                                             size_t src_stride, size_t dst_stride) {
+  src += (size_t)blockIdx.y * src_stride;  // chunk blockIdx.y of a batch
+  dst += (size_t)blockIdx.y * dst_stride;
+  const int lane = threadIdx.x & 63;
+  const size_t tb = (size_t)blockIdx.x * DE_V * 16 * MC_BLOCK;
+  mc_u32x4 x[DE_V];
+  uint32_t q_lo[DE_V], q_hi[DE_V];  // lane 0: the 8 bytes before its vector
+#pragma unroll
+  for (int r = 0; r < DE_V; ++r) {
+    const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
+    if (off + 16 <= nbytes) {
+      x[r] = mc_ld16<true>(src + off);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 16 && off + j < nbytes; ++j) w[j >> 2] |= (uint32_t)src[off + j] << (8 * (j & 3));
+      x[r] = mc_u32x4{w[0], w[1], w[2], w[3]};
+    }
+    q_lo[r] = q_hi[r] = 0;
+    if (lane == 0 && off < nbytes && off > 0) {
+      q_hi[r] = *reinterpret_cast<const uint32_t *>(src + off - 4);
+      if (ES == 8) q_lo[r] = *reinterpret_cast<const uint32_t *>(src + off - 8);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < DE_V; ++r) {
+    const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
+    uint32_t p_hi = __shfl_up(x[r].w, 1, 64), p_lo = __shfl_up(x[r].z, 1, 64);
+    if (lane == 0) {
+      p_hi = q_hi[r];
+      p_lo = q_lo[r];
+    }
+    const mc_u32x4 y = delta_vec<ES>(x[r], p_lo, p_hi);
+    if (off + 16 <= nbytes) {
+      mc_st16<true>(dst + off, y);
+    } else if (off < nbytes) {
+      const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+      for (int j = 0; j < 16 && off + j < nbytes; ++j) dst[off + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host dispatch
 // ---------------------------------------------------------------------------
@@ -330,6 +417,15 @@ int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, dou
   return launch_map<K_QUANTIZE>(src, dst, n, p, (hipStream_t)stream);
 }
 
+// MCODEC_DELTA_ENC_VEC=0 keeps same-width integer encodes on k_delta_enc (A/B)
+static bool delta_enc_vec_enabled() {
+  static const bool b = [] {
+    const char *e = getenv("MCODEC_DELTA_ENC_VEC");
+    return !(e && atoi(e) == 0);
+  }();
+  return b;
+}
+
 int mc_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype,
                     mc_stream_t stream) {
   return mc_delta_encode_batch(src, 0, dst, 0, 1, n, dtype, astype, stream);
@@ -347,6 +443,8 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
   uint8_t *d = static_cast<uint8_t *>(dst);
   const bool vec = aligned_for(src, ss) && aligned_for(dst, ds) &&
                    (nchunks == 1 || (src_stride % (4 * ss) == 0 && dst_stride % (4 * ds) == 0));
+  const bool al16 = (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
+                    (nchunks == 1 || (src_stride % 16 == 0 && dst_stride % 16 == 0));
   constexpr size_t YMAX = 65535;
   for (size_t c0 = 0; c0 < nchunks; c0 += YMAX) {
     const dim3 grid(blocks_for(n), (unsigned)min(YMAX, nchunks - c0));
@@ -355,7 +453,14 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
     // same-width integers: wrapping differences have the same bits whatever
     // the signedness, so every such pair runs the signed instantiation
     const int same = (dtype == astype && dtype != MC_B1 && !mc_is_float(dtype)) ? ss : 0;
-    if (vec && same == 1)
+    if (same && al16 && delta_enc_vec_enabled()) {
+      const size_t per = (size_t)DE_V * 16 * MC_BLOCK;
+      const dim3 g2((unsigned)((n * ss + per - 1) / per), grid.y);
+      if (same == 1) k_delta_enc_same<1><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n, src_stride, dst_stride);
+      else if (same == 2) k_delta_enc_same<2><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 2, src_stride, dst_stride);
+      else if (same == 4) k_delta_enc_same<4><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 4, src_stride, dst_stride);
+      else k_delta_enc_same<8><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 8, src_stride, dst_stride);
+    } else if (vec && same == 1)
       k_delta_enc<MC_I1, MC_I1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I1, MC_I1, src_stride, dst_stride);
     else if (vec && same == 2)
       k_delta_enc<MC_I2, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I2, MC_I2, src_stride, dst_stride);
