@@ -71,6 +71,30 @@ __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ sr
   const int a = A_ >= 0 ? A_ : prm.a;
   const int ss = mc_itemsize(d), ds = mc_itemsize(a);
   const size_t base = (size_t)blockIdx.x * ELEMS_PER_BLOCK;
+  auto op = [&](uint64_t e) {
+    return mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e, d), d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a);
+  };
+  if (VEC && base + ELEMS_PER_BLOCK <= n) {
+    // whole block in range: every load of the block issued before any store
+    constexpr int NS = EPL == 2 ? 2 * STEPS : STEPS;
+    uint64_t e[NS][EPL];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const size_t i0 = base + (size_t)s * EPL * MC_BLOCK + EPL * (size_t)threadIdx.x;
+      if constexpr (EPL == 2) mc_load2(src + i0 * ss, ss, e[s]);
+      else mc_load4(src + i0 * ss, ss, e[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const size_t i0 = base + (size_t)s * EPL * MC_BLOCK + EPL * (size_t)threadIdx.x;
+      uint64_t o[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) o[k] = op(e[s][k]);
+      if constexpr (EPL == 2) mc_store2(dst + i0 * ds, ds, o);
+      else mc_store4(dst + i0 * ds, ds, o);
+    }
+    return;
+  }
   if constexpr (VEC && EPL == 2) {
 #pragma unroll
     for (int s = 0; s < 2 * STEPS; ++s) {
@@ -122,6 +146,34 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitround(const uint8_t *__restrict
                                                        uint8_t *__restrict__ dst, size_t nbytes,
                                                        McBitRound br, bool vec) {
   const size_t base = (size_t)blockIdx.x * (16 * STEPS * MC_BLOCK);
+  auto round4 = [&](mc_u32x4 v) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (ES == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = mc_bitround16x2(w[k], br);
+    } else if constexpr (ES == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = mc_bitround32(w[k], br);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint64_t r = mc_bitround64(((uint64_t)w[2 * k + 1] << 32) | w[2 * k], br);
+        w[2 * k] = (uint32_t)r;
+        w[2 * k + 1] = (uint32_t)(r >> 32);
+      }
+    }
+    return mc_u32x4{w[0], w[1], w[2], w[3]};
+  };
+  if (vec && base + 16 * STEPS * MC_BLOCK <= nbytes) {
+    // whole block in range: every load issued before any store
+    mc_u32x4 v[STEPS];
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) v[s] = mc_ld16<true>(src + base + ((size_t)s * MC_BLOCK + threadIdx.x) * 16);
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s)
+      mc_st16<true>(dst + base + ((size_t)s * MC_BLOCK + threadIdx.x) * 16, round4(v[s]));
+    return;
+  }
   if (vec) {
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
