@@ -126,7 +126,13 @@ int mc_delta_encode(const void *src, void *dst, size_t n, int dtype,
                     int astype, mc_stream_t stream);
 /* dst = cumsum(dtype(src)) accumulated in dtype (bool: logical or).  Integer
  * dtypes use a parallel scan (modular arithmetic, bit-exact); float dtypes
- * keep numpy's sequential left-to-right rounding (serial per chunk). */
+ * keep numpy's sequential left-to-right rounding.  For f4/f8 with astype ==
+ * dtype, 16-B aligned buffers and the workspace this function asks for, a
+ * parallel scan is verified element by element against that recurrence and
+ * the serial chain reruns from the first mismatch (bit-exact for any data;
+ * smooth data verify entirely).  Otherwise (or with no workspace) float
+ * decode is the serial chain.  The workspace's last 8 bytes hold the index
+ * of the first mismatch (n if none) after the call. */
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
                     int dtype, void *workspace, size_t workspace_bytes,

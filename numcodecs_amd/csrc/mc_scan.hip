@@ -167,7 +167,8 @@ template <int A_, int D, bool VEC, int SER_SLOT_BYTES = 32768, int SER_G = 16>
 __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__ src,
                                                      size_t src_stride,
                                                      uint8_t *__restrict__ dst,
-                                                     size_t dst_stride, size_t n, int a_rt) {
+                                                     size_t dst_stride, size_t n, int a_rt,
+                                                     const uint64_t *__restrict__ startp = nullptr) {
   using T = typename SerAcc<D>::T;
   constexpr int BLK = SER_SLOT_BYTES / (int)sizeof(T);
   constexpr int DS = D == MC_F8 ? 8 : (D == MC_F4 ? 4 : 2);
@@ -176,6 +177,27 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
   const int as = mc_itemsize(a);
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
+  // fix-up mode (single chunk, after k_fspec_apply): the chain restarts at
+  // the first element whose speculative value failed verification (rounded
+  // down to a multiple of 4 so vector accesses stay aligned), carrying the
+  // verified value before it; nothing to do if every element verified
+  bool has_carry = false;
+  T carry = 0;
+  if (startp) {
+    size_t s0 = (size_t)*startp;
+    if (s0 >= n) return;
+    s0 &= ~(size_t)3;
+    if (s0 > 0) {
+      has_carry = true;
+      const uint64_t cb = mc_load_elem_u(dst, s0 - 1, DS);
+      if constexpr (D == MC_F8) carry = __builtin_bit_cast(double, cb);
+      else if constexpr (D == MC_F4) carry = __builtin_bit_cast(float, (uint32_t)cb);
+      else carry = (T)mc_num_from_bits(cb, D).f;
+    }
+    src += s0 * as;
+    dst += s0 * DS;
+    n -= s0;
+  }
   const int lane = threadIdx.x & 63;
   const bool io = threadIdx.x >= 64;
   const size_t nb = (n + BLK - 1) / BLK;
@@ -240,7 +262,8 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
       const int cnt = (int)min((size_t)BLK, n - b * BLK);
       int j = 0;
       if (b == 0) {  // out[0] = x[0] exactly (no add), then align to a group
-        acc = p[0];
+        acc = has_carry ? ser_add<D>(carry, p[0]) : p[0];
+        p[0] = acc;
         const int m = cnt < SER_G ? cnt : SER_G;
         for (int k = 1; k < m; ++k) {
           acc = ser_add<D>(acc, p[k]);
@@ -695,12 +718,219 @@ static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, h
   k_dscan_apply<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, group, part);
 }
 
+
+// ---------------------------------------------------------------------------
+// Speculative float Delta decode (one chunk, astype == dtype in {f4, f8}).
+// numpy's cumsum rounds after every add, so in general the adds form one
+// serial chain.  But when every add happens to be exact -- the common case
+// for the output of a Delta encode of slowly varying values, where each
+// difference is exact (Sterbenz) and adding it back is exact too -- the
+// serial result IS the exact prefix sum, which a parallel scan computes.
+// So the decode speculates and verifies:
+//   1. k_fspec_reduce: per-tile total of the tile's prefix sums in double,
+//      with the same block-scan code as the apply pass, so a tile's total is
+//      bitwise the value its last element's candidate is built from;
+//   2. k_fspec_sums: exclusive scan of the totals (any order: each tile only
+//      uses its own prefix and its predecessor's) and reset of the
+//      first-failure word;
+//   3. k_fspec_apply: candidate c_i = dtype(S_tile + local prefix_i); every
+//      element checks c_i == dtype(c_{i-1} + enc_i) bitwise -- numpy's
+//      recurrence itself -- with non-finite values counted as failures, and
+//      the smallest failing index goes to one word (atomicMin; tiles past a
+//      recorded failure skip their work);
+//   4. k_scan_serial in fix-up mode reruns the serial chain from that index
+//      with the verified value before it (returns at once when nothing
+//      failed).
+// The candidates are a deterministic function of the input, so the first
+// failure is always recorded, and by induction from c_0 = enc_0 every
+// element before it equals numpy's serial value; after it the chain is
+// serial again.  The output is bit-exact for any input; the data only decide
+// how much of the chunk runs at scan speed instead of one add per element.
+// ---------------------------------------------------------------------------
+constexpr int FS_PER = 8;  // consecutive elements per thread
+constexpr size_t FS_TILE = (size_t)FS_PER * MC_BLOCK;
+
+template <typename T>
+MC_DEV void fs_load(const uint8_t *src, size_t n, size_t e0, T (&v)[FS_PER]) {
+  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int W = 16 / sizeof(T);
+  if (e0 + FS_PER <= n) {
+    const vec *p = reinterpret_cast<const vec *>(src + e0 * sizeof(T));
+#pragma unroll
+    for (int u = 0; u < FS_PER / W; ++u) {
+      const vec x = __builtin_nontemporal_load(p + u);
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[u * W + e] = x[e];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < FS_PER; ++k) v[k] = e0 + k < n ? reinterpret_cast<const T *>(src)[e0 + k] : (T)0;
+  }
+}
+
+// q[k] = this thread's inclusive prefix sums in double, pre = the sum of the
+// tile's elements before the thread's first one.  Deterministic (fixed
+// association), shared by the reduce and apply passes.
+template <typename T>
+MC_DEV void fs_tile_scan(const T (&v)[FS_PER], double (&q)[FS_PER], double &pre,
+                         double (&lds)[MC_BLOCK / 64]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  q[0] = (double)v[0];
+#pragma unroll
+  for (int k = 1; k < FS_PER; ++k) q[k] = q[k - 1] + (double)v[k];
+  double incl = q[FS_PER - 1];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl = o + incl;
+  }
+  if (lane == 63) lds[wave] = incl;
+  const double ex = __shfl_up(incl, 1, 64);
+  __syncthreads();
+  double w = 0.0;
+  for (int j = 0; j < wave; ++j) w = w + lds[j];
+  pre = lane ? w + ex : w;
+}
+
+template <typename T>
+MC_DEV uint64_t fs_bits(T x) {
+  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(uint64_t, x);
+  else return __builtin_bit_cast(uint32_t, x);
+}
+
+template <typename T>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n,
+                                                          double *__restrict__ sums) {
+  __shared__ double lds[MC_BLOCK / 64];
+  T v[FS_PER];
+  fs_load<T>(src, n, (size_t)blockIdx.x * FS_TILE + (size_t)threadIdx.x * FS_PER, v);
+  double q[FS_PER], pre;
+  fs_tile_scan<T>(v, q, pre, lds);
+  if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = pre + q[FS_PER - 1];
+}
+
+// exclusive scan of the tile totals by one workgroup (contiguous runs per
+// thread, block scan of the run totals), and the first-failure word := n
+__global__ __launch_bounds__(1024) void k_fspec_sums(const double *__restrict__ sums,
+                                                     double *__restrict__ pre, size_t ntiles,
+                                                     uint64_t *__restrict__ fail, size_t n) {
+  __shared__ double lds[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t per = (ntiles + 1023) / 1024;
+  const size_t b = (size_t)threadIdx.x * per, e = min(b + per, ntiles);
+  double r = 0.0;
+  for (size_t i = b; i < e; ++i) r += sums[i];
+  double incl = r;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl = o + incl;
+  }
+  if (lane == 63) lds[wave] = incl;
+  const double ex = __shfl_up(incl, 1, 64);
+  __syncthreads();
+  double run = 0.0;
+  for (int j = 0; j < wave; ++j) run += lds[j];
+  if (lane) run += ex;
+  for (size_t i = b; i < e; ++i) {
+    pre[i] = run;
+    run += sums[i];
+  }
+  if (threadIdx.x == 0) *fail = n;
+}
+
+template <typename T>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restrict__ src,
+                                                         uint8_t *__restrict__ dst, size_t n,
+                                                         const double *__restrict__ sums,
+                                                         const double *__restrict__ pre_t,
+                                                         uint64_t *__restrict__ fail) {
+  __shared__ double lds[MC_BLOCK / 64];
+  __shared__ T ldsc[MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t tile = blockIdx.x;
+  const size_t t0 = tile * FS_TILE;
+  // a tile at or past a recorded failure is recomputed by the serial fix-up
+  if (__builtin_nontemporal_load(fail) <= t0) return;
+  const size_t e0 = t0 + (size_t)threadIdx.x * FS_PER;
+  T v[FS_PER];
+  fs_load<T>(src, n, e0, v);
+  double q[FS_PER], pre;
+  fs_tile_scan<T>(v, q, pre, lds);
+  const double S = pre_t[tile];
+  T c[FS_PER];
+#pragma unroll
+  for (int k = 0; k < FS_PER; ++k) c[k] = (T)(S + (pre + q[k]));
+  const T up = __shfl_up(c[FS_PER - 1], 1, 64);
+  if (lane == 63) ldsc[wave] = c[FS_PER - 1];
+  __syncthreads();
+  T p0;
+  if (threadIdx.x == 0) p0 = tile ? (T)(pre_t[tile - 1] + sums[tile - 1]) : (T)0;
+  else if (lane == 0) p0 = ldsc[wave - 1];
+  else p0 = up;
+  uint64_t first = ~(uint64_t)0;
+#pragma unroll
+  for (int k = FS_PER - 1; k >= 0; --k) {  // descending: the last write is the smallest
+    const size_t g = e0 + k;
+    const T pv = k ? c[k - 1] : p0;
+    const T r = g == 0 ? v[0] : (T)(pv + v[k]);
+    const bool ok = fs_bits<T>(c[k]) == fs_bits<T>(r) && __builtin_isfinite(c[k]) && __builtin_isfinite(v[k]);
+    if (g < n && !ok) first = g;
+  }
+  if (e0 + FS_PER <= n) {
+    typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+    constexpr int W = 16 / sizeof(T);
+    vec *p = reinterpret_cast<vec *>(dst + e0 * sizeof(T));
+#pragma unroll
+    for (int u = 0; u < FS_PER / W; ++u) {
+      vec x;
+#pragma unroll
+      for (int e = 0; e < W; ++e) x[e] = c[u * W + e];
+      __builtin_nontemporal_store(x, p + u);
+    }
+  } else {
+    for (int k = 0; k < FS_PER && e0 + k < n; ++k) reinterpret_cast<T *>(dst)[e0 + k] = c[k];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(first, off, 64);
+    first = o < first ? o : first;
+  }
+  if (lane == 0 && first != ~(uint64_t)0) atomicMin((unsigned long long *)fail, (unsigned long long)first);
+}
+
+// MCODEC_FSPEC=0 disables the speculative float path (A/B: serial only)
+static bool fspec_enabled() {
+  static const bool b = [] {
+    const char *e = getenv("MCODEC_FSPEC");
+    return !(e && atoi(e) == 0);
+  }();
+  return b;
+}
+
+static size_t fspec_ws_bytes(size_t n) {
+  const size_t ntiles = (n + FS_TILE - 1) / FS_TILE;
+  return (2 * ntiles + 1) * sizeof(uint64_t);
+}
+
+template <int D>
+static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipStream_t st) {
+  using T = typename std::conditional<D == MC_F8, double, float>::type;
+  const size_t ntiles = (n + FS_TILE - 1) / FS_TILE;
+  double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
+  uint64_t *fail = reinterpret_cast<uint64_t *>(pre + ntiles);
+  k_fspec_reduce<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, sums);
+  k_fspec_sums<<<1, 1024, 0, st>>>(sums, pre, ntiles, fail, n);
+  k_fspec_apply<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, sums, pre, fail);
+  k_scan_serial<D, D, true, 32768, 32><<<1, 128, 0, st>>>(s, 0, d, 0, n, D, fail);
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
-  if (mc_is_float(dtype)) return 0;
+  if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n) : 0;
   const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
   const size_t fast = astype == dtype && dtype != MC_B1 ? dscan_ws_entries(n, mc_itemsize(dtype)) : 0;
   return (generic > fast ? generic : fast) * sizeof(uint64_t);
@@ -715,6 +945,16 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   if (mc_is_float(dtype)) {
+    // speculative parallel scan + verification, serial fix-up (above); the
+    // plain serial chain where the preconditions (workspace, alignment,
+    // astype == dtype, f4/f8) do not hold
+    if (astype == dtype && dtype != MC_F2 && fspec_enabled() && workspace &&
+        workspace_bytes >= fspec_ws_bytes(n) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
+        (uintptr_t)workspace % 8 == 0) {
+      if (dtype == MC_F8) launch_fspec<MC_F8>(s, d, n, workspace, st);
+      else launch_fspec<MC_F4>(s, d, n, workspace, st);
+      return mc_last_launch();
+    }
     launch_serial_any(s, 0, d, 0, n, 1, astype, dtype, st);
     return mc_last_launch();
   }

@@ -1,0 +1,157 @@
+"""Speculative float Delta decode (mc_scan.hip k_fspec_*): one f4/f8 chunk is
+decoded by a parallel prefix sum whose every element is checked against
+numpy's serial recurrence (delta.py:69-83, np.cumsum); the serial chain
+reruns from the first element that fails.  The output must be bit-identical
+to the oracle whatever the data, and for smooth data (every add exact) the
+whole chunk must verify, so the fix-up launch has nothing to do.
+"""
+
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from numcodecs_amd import Delta, _native, _ops
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(1016)
+TILE = 2048  # FS_TILE: 8 elements x 256 threads
+
+
+def _oracle_dec(enc, dt):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return oracle.delta_decode(enc, dt, dt)
+
+
+def _oracle_enc(x, dt):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return oracle.delta_encode(x, dt, dt)
+
+
+def _smooth(dt, n, kind):
+    i = np.arange(n, dtype=np.float64)
+    if kind == "ramp":
+        x = 1000.0 + 0.25 * i
+    elif kind == "sine":  # slowly varying, every difference exact (Sterbenz)
+        x = 5000.0 + 100.0 * np.sin(2 * np.pi * i / 65536.0)
+    else:  # integers stored as floats
+        x = np.floor(i / 3.0) - 7.0 * (i % 5)
+    return x.astype(dt)
+
+
+def _decode_raw(enc_np, dt):
+    """mc_delta_decode through the C ABI with our own workspace: returns
+    (decoded array, first-failure word)."""
+    dev = torch.device("cuda", 0)
+    n = enc_np.size
+    src = torch.from_numpy(enc_np).to(dev)
+    dst = torch.empty_like(src)
+    a = _ops.dtype_code(dt)
+    ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
+    ntiles = (n + TILE - 1) // TILE
+    assert ws_n == (2 * ntiles + 1) * 8
+    ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
+    _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
+                                              _ops.stream(src)), "mc_delta_decode")
+    torch.cuda.synchronize()
+    return dst.cpu().numpy(), int(ws[-1].item())
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("kind", ["ramp", "sine", "ints"])
+@pytest.mark.parametrize("n", [1, 5, 2047, 2048, 2049, 100003, (1 << 20) + 3])
+def test_smooth_data_verifies_whole_chunk(device, dt, kind, n):
+    x = _smooth(dt, n, kind)
+    enc = _oracle_enc(x, dt)
+    got, first_fail = _decode_raw(enc, dt)
+    ref = _oracle_dec(enc, dt)
+    assert got.tobytes() == ref.tobytes()
+    assert first_fail == n, f"speculation failed at {first_fail} of {n}"
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("pos", [0, 1, 2, 3, 4, 5, 2046, 2047, 2048, 2049, 6143, 50001, 99999, 100002])
+def test_rounding_event_mid_chunk(device, dt, pos):
+    """An inexact add at `pos`.  Whether the candidates after it still verify
+    depends on the data (a later rounding of the exact sum may or may not
+    agree with the chain); either way the output must equal numpy's."""
+    n = 100003
+    enc = _oracle_enc(_smooth(dt, n, "ramp"), dt)
+    enc[pos] = np.asarray(0.1, dtype=dt)  # 1000.25*k + 0.1 is not representable
+    got, _ = _decode_raw(enc, dt)
+    assert got.tobytes() == _oracle_dec(enc, dt).tobytes()
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("special", ["nan", "inf", "-inf", "negzero_first", "negzero_mid", "tiny", "huge"])
+def test_special_values(device, dt, special):
+    n = 3 * TILE + 17
+    enc = _oracle_enc(_smooth(dt, n, "ints"), dt)
+    fi = np.finfo(dt)
+    if special == "nan":
+        enc[4000] = np.nan
+    elif special == "inf":
+        enc[4001] = np.inf
+    elif special == "-inf":
+        enc[2048] = -np.inf
+    elif special == "negzero_first":
+        enc[0] = -0.0
+    elif special == "negzero_mid":
+        enc[3000] = -0.0
+    elif special == "tiny":
+        enc[1234] = fi.tiny / 8  # subnormal
+    else:  # overflows the running sum
+        enc[5000] = fi.max
+        enc[5001] = fi.max
+    got, _ = _decode_raw(enc, dt)
+    ref = _oracle_dec(enc, dt)
+    if special == "nan":  # NaN payloads are not pinned (test_gpu_delta.py)
+        assert got[:4000].tobytes() == ref[:4000].tobytes()
+        assert np.isnan(got[4000:]).all() and np.isnan(ref[4000:]).all()
+    else:
+        assert got.tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+def test_random_data_falls_back_to_serial(device, dt):
+    enc = RNG.normal(0, 1, 3 * TILE * 7 + 5).astype(dt)
+    got, first_fail = _decode_raw(enc, dt)
+    assert got.tobytes() == _oracle_dec(enc, dt).tobytes()
+    assert first_fail < enc.size
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+def test_codec_roundtrip_smooth_4m(device, dt):
+    """Delta(dt) encode + decode through the codec API on 4 Mi smooth values."""
+    x = _smooth(dt, 1 << 22, "sine")
+    xd = torch.from_numpy(x).to(device)
+    enc = Delta(dt).encode(xd)
+    assert enc.cpu().numpy().tobytes() == _oracle_enc(x, dt).tobytes()
+    dec = Delta(dt).decode(enc)
+    assert dec.cpu().numpy().tobytes() == x.tobytes()
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+def test_repeated_calls_reset_failure_word(device, dt):
+    """The failure word lives in the workspace: a verified call after a
+    failing one (same workspace) must not inherit the old index."""
+    dev = torch.device("cuda", 0)
+    n = 10 * TILE
+    good = _oracle_enc(_smooth(dt, n, "ramp"), dt)
+    bad = good.copy()
+    bad[7] = np.inf  # non-finite: always a verification failure
+    a = _ops.dtype_code(dt)
+    ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
+    ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
+    for enc in (bad, good, bad, good):
+        src = torch.from_numpy(enc).to(dev)
+        dst = torch.empty_like(src)
+        _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
+                                                  _ops.stream(src)), "mc_delta_decode")
+        assert dst.cpu().numpy().tobytes() == _oracle_dec(enc, dt).tobytes()
+        assert int(ws[-1].item()) == (n if enc is good else 7)

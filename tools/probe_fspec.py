@@ -1,0 +1,58 @@
+"""Float Delta decode of one chunk: speculative scan (default) vs the serial
+chain (MCODEC_FSPEC=0 in a child), smooth data (every add exact) and random
+data (verification fails early, serial fix-up).  Rotating buffers; prints one
+JSON line.  Usage: python tools/probe_fspec.py"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from numcodecs_amd import Delta  # noqa: E402
+
+
+def time_decode(dt, n, kind, reps=10, rot=3):
+    dev = torch.device("cuda", 0)
+    i = torch.arange(n, device=dev, dtype=torch.float64)
+    if kind == "smooth":
+        x = (5000.0 + 100.0 * torch.sin(2 * np.pi * i / 65536.0)).to(getattr(torch, {"<f4": "float32", "<f8": "float64"}[dt]))
+    else:
+        x = torch.randn(n, device=dev, dtype=getattr(torch, {"<f4": "float32", "<f8": "float64"}[dt]))
+    codec = Delta(dt)
+    encs = [codec.encode(x) for _ in range(rot)]
+    dec = codec.decode(encs[0])
+    assert kind != "smooth" or torch.equal(dec, x)
+    torch.cuda.synchronize()
+    ts = []
+    for r in range(reps):
+        e = encs[r % rot]
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        codec.decode(e)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    us = float(np.median(ts))
+    nbytes = n * np.dtype(dt).itemsize
+    return {"us": round(us, 1), "GBps_2N": round(2 * nbytes / us / 1e3, 2)}
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "serial":
+        os.environ["MCODEC_FSPEC"] = "0"
+        out = {}
+        for dt in ("<f4", "<f8"):
+            out[f"serial_{dt}_16MiB_smooth"] = time_decode(dt, (16 << 20) // np.dtype(dt).itemsize, "smooth", reps=3)
+        print(json.dumps(out))
+        sys.exit(0)
+    # the serial leg runs in a child started before this process touches the GPU
+    r = subprocess.run([sys.executable, __file__, "serial"], capture_output=True, text=True, timeout=300)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for dt in ("<f4", "<f8"):
+        for mib in (16, 256):
+            out[f"spec_{dt}_{mib}MiB_smooth"] = time_decode(dt, (mib << 20) // np.dtype(dt).itemsize, "smooth")
+        out[f"spec_{dt}_16MiB_random"] = time_decode(dt, (16 << 20) // np.dtype(dt).itemsize, "random", reps=3)
+    print(json.dumps(out))
