@@ -747,49 +747,82 @@ static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, h
 // serial again.  The output is bit-exact for any input; the data only decide
 // how much of the chunk runs at scan speed instead of one add per element.
 // ---------------------------------------------------------------------------
-constexpr int FS_PER = 8;  // consecutive elements per thread
-constexpr size_t FS_TILE = (size_t)FS_PER * MC_BLOCK;
+// A thread holds FS_Q 16-B vectors (FS_W elements each) in FS_Q segments of
+// the tile: segment q is 16*MC_BLOCK contiguous bytes and thread t owns its
+// vector at 16*t, so every wave load/store covers 1 KiB contiguously; 16 KiB
+// per tile (4096 f4 / 2048 f8 elements).
+template <typename T> constexpr int fs_w() { return 16 / (int)sizeof(T); }
+constexpr int FS_Q = 4;
+template <typename T> constexpr size_t fs_tile() { return (size_t)fs_w<T>() * FS_Q * MC_BLOCK; }
 
 template <typename T>
-MC_DEV void fs_load(const uint8_t *src, size_t n, size_t e0, T (&v)[FS_PER]) {
-  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
-  constexpr int W = 16 / sizeof(T);
-  if (e0 + FS_PER <= n) {
-    const vec *p = reinterpret_cast<const vec *>(src + e0 * sizeof(T));
+MC_DEV size_t fs_elem0(size_t t0, int q) {  // first element of this thread's vector in segment q
+  return t0 + (size_t)q * fs_w<T>() * MC_BLOCK + (size_t)threadIdx.x * fs_w<T>();
+}
+
+template <typename T>
+MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, T (&v)[FS_Q][fs_w<T>()]) {
+  typedef T vec __attribute__((ext_vector_type(fs_w<T>())));
+  constexpr int W = fs_w<T>();
 #pragma unroll
-    for (int u = 0; u < FS_PER / W; ++u) {
-      const vec x = __builtin_nontemporal_load(p + u);
+  for (int q = 0; q < FS_Q; ++q) {
+    const size_t e0 = fs_elem0<T>(t0, q);
+    if (e0 + W <= n) {
+      const vec x = __builtin_nontemporal_load(reinterpret_cast<const vec *>(src + e0 * sizeof(T)));
 #pragma unroll
-      for (int e = 0; e < W; ++e) v[u * W + e] = x[e];
+      for (int e = 0; e < W; ++e) v[q][e] = x[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = e0 + e < n ? reinterpret_cast<const T *>(src)[e0 + e] : (T)0;
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < FS_PER; ++k) v[k] = e0 + k < n ? reinterpret_cast<const T *>(src)[e0 + k] : (T)0;
   }
 }
 
-// q[k] = this thread's inclusive prefix sums in double, pre = the sum of the
-// tile's elements before the thread's first one.  Deterministic (fixed
-// association), shared by the reduce and apply passes.
+// p[q][e] = the tile-relative inclusive prefix sum (double) of this thread's
+// element e of segment q.  Fixed association (element, lane, wave, segment
+// order), so the reduce and apply passes compute bitwise the same values.
 template <typename T>
-MC_DEV void fs_tile_scan(const T (&v)[FS_PER], double (&q)[FS_PER], double &pre,
-                         double (&lds)[MC_BLOCK / 64]) {
+MC_DEV void fs_tile_scan(const T (&v)[FS_Q][fs_w<T>()], double (&p)[FS_Q][fs_w<T>()],
+                         double (&lds)[FS_Q][MC_BLOCK / 64]) {
+  constexpr int W = fs_w<T>();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  q[0] = (double)v[0];
+  double incl[FS_Q];
 #pragma unroll
-  for (int k = 1; k < FS_PER; ++k) q[k] = q[k - 1] + (double)v[k];
-  double incl = q[FS_PER - 1];
+  for (int q = 0; q < FS_Q; ++q) {
+    p[q][0] = (double)v[q][0];
+#pragma unroll
+    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (double)v[q][e];
+    incl[q] = p[q][W - 1];
+  }
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const double o = __shfl_up(incl, off, 64);
-    if (lane >= off) incl = o + incl;
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const double o = __shfl_up(incl[q], off, 64);
+      if (lane >= off) incl[q] = o + incl[q];
+    }
   }
-  if (lane == 63) lds[wave] = incl;
-  const double ex = __shfl_up(incl, 1, 64);
+  double ex[FS_Q];
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    if (lane == 63) lds[q][wave] = incl[q];
+    ex[q] = __shfl_up(incl[q], 1, 64);
+  }
   __syncthreads();
-  double w = 0.0;
-  for (int j = 0; j < wave; ++j) w = w + lds[j];
-  pre = lane ? w + ex : w;
+  double base = 0.0;
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    double w = 0.0, tot = 0.0;
+#pragma unroll
+    for (int j = 0; j < MC_BLOCK / 64; ++j) {
+      if (j < wave) w = w + lds[q][j];
+      tot = tot + lds[q][j];
+    }
+    const double pre = base + (lane ? w + ex[q] : w);
+#pragma unroll
+    for (int e = 0; e < W; ++e) p[q][e] = pre + p[q][e];
+    base = base + tot;
+  }
 }
 
 template <typename T>
@@ -801,40 +834,72 @@ MC_DEV uint64_t fs_bits(T x) {
 template <typename T>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n,
                                                           double *__restrict__ sums) {
-  __shared__ double lds[MC_BLOCK / 64];
-  T v[FS_PER];
-  fs_load<T>(src, n, (size_t)blockIdx.x * FS_TILE + (size_t)threadIdx.x * FS_PER, v);
-  double q[FS_PER], pre;
-  fs_tile_scan<T>(v, q, pre, lds);
-  if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = pre + q[FS_PER - 1];
+  constexpr int W = fs_w<T>();
+  __shared__ double lds[FS_Q][MC_BLOCK / 64];
+  T v[FS_Q][W];
+  fs_load<T>(src, n, (size_t)blockIdx.x * fs_tile<T>(), v);
+  double p[FS_Q][W];
+  fs_tile_scan<T>(v, p, lds);
+  if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = p[FS_Q - 1][W - 1];
 }
 
-// exclusive scan of the tile totals by one workgroup (contiguous runs per
-// thread, block scan of the run totals), and the first-failure word := n
+// exclusive scan of the tile totals by one workgroup, in rounds of
+// 1024 x FS_SR totals staged through LDS: coalesced loads into LDS, each
+// thread scans FS_SR consecutive totals in registers, one wave scan of the
+// thread totals and one LDS exchange of the wave totals, prefixes written
+// back through LDS and stored coalesced.  (Scanning 64 values per wave step
+// instead costs 16x more cross-lane shuffles, all through one CU's LDS
+// crossbar: 16 us for 16 Ki tiles.)  Also sets the first-failure word := n.
+constexpr int FS_SR = 4;
 __global__ __launch_bounds__(1024) void k_fspec_sums(const double *__restrict__ sums,
                                                      double *__restrict__ pre, size_t ntiles,
                                                      uint64_t *__restrict__ fail, size_t n) {
+  __shared__ double stage[1024 * FS_SR];
   __shared__ double lds[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t per = (ntiles + 1023) / 1024;
-  const size_t b = (size_t)threadIdx.x * per, e = min(b + per, ntiles);
-  double r = 0.0;
-  for (size_t i = b; i < e; ++i) r += sums[i];
-  double incl = r;
+  double carry = 0.0;
+  for (size_t r0 = 0; r0 < ntiles; r0 += (size_t)1024 * FS_SR) {
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double o = __shfl_up(incl, off, 64);
-    if (lane >= off) incl = o + incl;
-  }
-  if (lane == 63) lds[wave] = incl;
-  const double ex = __shfl_up(incl, 1, 64);
-  __syncthreads();
-  double run = 0.0;
-  for (int j = 0; j < wave; ++j) run += lds[j];
-  if (lane) run += ex;
-  for (size_t i = b; i < e; ++i) {
-    pre[i] = run;
-    run += sums[i];
+    for (int k = 0; k < FS_SR; ++k) {
+      const size_t i = r0 + (size_t)k * 1024 + threadIdx.x;
+      stage[k * 1024 + threadIdx.x] = i < ntiles ? sums[i] : 0.0;
+    }
+    __syncthreads();
+    double x[FS_SR];
+#pragma unroll
+    for (int k = 0; k < FS_SR; ++k) x[k] = stage[threadIdx.x * FS_SR + k];
+    double r = x[0];
+#pragma unroll
+    for (int k = 1; k < FS_SR; ++k) r += x[k];
+    double incl = r;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl = o + incl;
+    }
+    if (lane == 63) lds[wave] = incl;
+    const double ex = __shfl_up(incl, 1, 64);
+    __syncthreads();
+    double run = carry, tot = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < wave) run += lds[j];
+      tot += lds[j];
+    }
+    if (lane) run += ex;
+#pragma unroll
+    for (int k = 0; k < FS_SR; ++k) {
+      stage[threadIdx.x * FS_SR + k] = run;
+      run += x[k];
+    }
+    carry += tot;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FS_SR; ++k) {
+      const size_t i = r0 + (size_t)k * 1024 + threadIdx.x;
+      if (i < ntiles) pre[i] = stage[k * 1024 + threadIdx.x];
+    }
+    __syncthreads();  // stage and lds reused by the next round
   }
   if (threadIdx.x == 0) *fail = n;
 }
@@ -845,51 +910,61 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
                                                          const double *__restrict__ sums,
                                                          const double *__restrict__ pre_t,
                                                          uint64_t *__restrict__ fail) {
-  __shared__ double lds[MC_BLOCK / 64];
-  __shared__ T ldsc[MC_BLOCK / 64];
+  constexpr int W = fs_w<T>();
+  typedef T vec __attribute__((ext_vector_type(W)));
+  __shared__ double lds[FS_Q][MC_BLOCK / 64];
+  __shared__ T ldsc[FS_Q][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t tile = blockIdx.x;
-  const size_t t0 = tile * FS_TILE;
+  const size_t t0 = tile * fs_tile<T>();
   // a tile at or past a recorded failure is recomputed by the serial fix-up
   if (__builtin_nontemporal_load(fail) <= t0) return;
-  const size_t e0 = t0 + (size_t)threadIdx.x * FS_PER;
-  T v[FS_PER];
-  fs_load<T>(src, n, e0, v);
-  double q[FS_PER], pre;
-  fs_tile_scan<T>(v, q, pre, lds);
-  const double S = pre_t[tile];
-  T c[FS_PER];
+  T v[FS_Q][W];
+  fs_load<T>(src, n, t0, v);
+  double p[FS_Q][W];
+  fs_tile_scan<T>(v, p, lds);
+  const double S = pre_t[tile];  // the tile's prefix
+  T c[FS_Q][W], up[FS_Q];
 #pragma unroll
-  for (int k = 0; k < FS_PER; ++k) c[k] = (T)(S + (pre + q[k]));
-  const T up = __shfl_up(c[FS_PER - 1], 1, 64);
-  if (lane == 63) ldsc[wave] = c[FS_PER - 1];
+  for (int q = 0; q < FS_Q; ++q) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) c[q][e] = (T)(S + p[q][e]);
+    up[q] = __shfl_up(c[q][W - 1], 1, 64);
+    if (lane == 63) ldsc[q][wave] = c[q][W - 1];
+  }
   __syncthreads();
-  T p0;
-  if (threadIdx.x == 0) p0 = tile ? (T)(pre_t[tile - 1] + sums[tile - 1]) : (T)0;
-  else if (lane == 0) p0 = ldsc[wave - 1];
-  else p0 = up;
+  // the tile's last candidate in the previous tile: the same double sum it
+  // was rounded from there (sums[] is that tile's last prefix, bitwise)
+  const T pbound = tile ? (T)(pre_t[tile - 1] + sums[tile - 1]) : (T)0;
   uint64_t first = ~(uint64_t)0;
 #pragma unroll
-  for (int k = FS_PER - 1; k >= 0; --k) {  // descending: the last write is the smallest
-    const size_t g = e0 + k;
-    const T pv = k ? c[k - 1] : p0;
-    const T r = g == 0 ? v[0] : (T)(pv + v[k]);
-    const bool ok = fs_bits<T>(c[k]) == fs_bits<T>(r) && __builtin_isfinite(c[k]) && __builtin_isfinite(v[k]);
-    if (g < n && !ok) first = g;
-  }
-  if (e0 + FS_PER <= n) {
-    typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
-    constexpr int W = 16 / sizeof(T);
-    vec *p = reinterpret_cast<vec *>(dst + e0 * sizeof(T));
+  for (int q = FS_Q - 1; q >= 0; --q) {  // descending: the last hit is the smallest index
+    T p0;
+    if (lane) p0 = up[q];
+    else if (wave) p0 = ldsc[q][wave - 1];
+    else p0 = q ? ldsc[q - 1][MC_BLOCK / 64 - 1] : pbound;
+    const size_t e0 = fs_elem0<T>(t0, q);
 #pragma unroll
-    for (int u = 0; u < FS_PER / W; ++u) {
+    for (int e = W - 1; e >= 0; --e) {
+      const size_t g = e0 + e;
+      const T pv = e ? c[q][e - 1] : p0;
+      const T r = g == 0 ? v[q][0] : (T)(pv + v[q][e]);
+      // a non-finite input makes its own prefix (and so c) non-finite
+      const bool ok = fs_bits<T>(c[q][e]) == fs_bits<T>(r) && __builtin_isfinite(c[q][e]);
+      if (g < n && !ok) first = g;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    const size_t e0 = fs_elem0<T>(t0, q);
+    if (e0 + W <= n) {
       vec x;
 #pragma unroll
-      for (int e = 0; e < W; ++e) x[e] = c[u * W + e];
-      __builtin_nontemporal_store(x, p + u);
+      for (int e = 0; e < W; ++e) x[e] = c[q][e];
+      __builtin_nontemporal_store(x, reinterpret_cast<vec *>(dst + e0 * sizeof(T)));
+    } else {
+      for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<T *>(dst)[e0 + e] = c[q][e];
     }
-  } else {
-    for (int k = 0; k < FS_PER && e0 + k < n; ++k) reinterpret_cast<T *>(dst)[e0 + k] = c[k];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -908,15 +983,18 @@ static bool fspec_enabled() {
   return b;
 }
 
-static size_t fspec_ws_bytes(size_t n) {
-  const size_t ntiles = (n + FS_TILE - 1) / FS_TILE;
-  return (2 * ntiles + 1) * sizeof(uint64_t);
+static size_t fspec_ntiles(size_t n, int dt) {
+  const size_t te = dt == MC_F8 ? fs_tile<double>() : fs_tile<float>();
+  return (n + te - 1) / te;
 }
+
+// tile totals, tile prefixes, the failure word
+static size_t fspec_ws_bytes(size_t n, int dt) { return (2 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
 
 template <int D>
 static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipStream_t st) {
   using T = typename std::conditional<D == MC_F8, double, float>::type;
-  const size_t ntiles = (n + FS_TILE - 1) / FS_TILE;
+  const size_t ntiles = fspec_ntiles(n, D);
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
   uint64_t *fail = reinterpret_cast<uint64_t *>(pre + ntiles);
   k_fspec_reduce<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, sums);
@@ -930,7 +1008,7 @@ static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipSt
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
-  if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n) : 0;
+  if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n, dtype) : 0;
   const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
   const size_t fast = astype == dtype && dtype != MC_B1 ? dscan_ws_entries(n, mc_itemsize(dtype)) : 0;
   return (generic > fast ? generic : fast) * sizeof(uint64_t);
@@ -949,7 +1027,7 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
     // plain serial chain where the preconditions (workspace, alignment,
     // astype == dtype, f4/f8) do not hold
     if (astype == dtype && dtype != MC_F2 && fspec_enabled() && workspace &&
-        workspace_bytes >= fspec_ws_bytes(n) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
+        workspace_bytes >= fspec_ws_bytes(n, dtype) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
         (uintptr_t)workspace % 8 == 0) {
       if (dtype == MC_F8) launch_fspec<MC_F8>(s, d, n, workspace, st);
       else launch_fspec<MC_F4>(s, d, n, workspace, st);

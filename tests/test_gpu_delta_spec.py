@@ -18,7 +18,11 @@ from numcodecs_amd import Delta, _native, _ops
 pytestmark = pytest.mark.gpu
 
 RNG = np.random.default_rng(1016)
-TILE = 2048  # FS_TILE: 8 elements x 256 threads
+TILE = 2048  # f8 tile (4 x 16-B vectors x 256 threads); the f4 tile is 4096
+
+
+def _tile(dt):
+    return 4096 if np.dtype(dt).itemsize == 4 else 2048
 
 
 def _oracle_dec(enc, dt):
@@ -53,7 +57,7 @@ def _decode_raw(enc_np, dt):
     dst = torch.empty_like(src)
     a = _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
-    ntiles = (n + TILE - 1) // TILE
+    ntiles = (n + _tile(dt) - 1) // _tile(dt)
     assert ws_n == (2 * ntiles + 1) * 8
     ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
     _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
@@ -64,7 +68,7 @@ def _decode_raw(enc_np, dt):
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])
 @pytest.mark.parametrize("kind", ["ramp", "sine", "ints"])
-@pytest.mark.parametrize("n", [1, 5, 2047, 2048, 2049, 100003, (1 << 20) + 3])
+@pytest.mark.parametrize("n", [1, 5, 1025, 2047, 2048, 2049, 4096, 4099, 100003, (1 << 20) + 3])
 def test_smooth_data_verifies_whole_chunk(device, dt, kind, n):
     x = _smooth(dt, n, kind)
     enc = _oracle_enc(x, dt)
@@ -75,7 +79,7 @@ def test_smooth_data_verifies_whole_chunk(device, dt, kind, n):
 
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])
-@pytest.mark.parametrize("pos", [0, 1, 2, 3, 4, 5, 2046, 2047, 2048, 2049, 6143, 50001, 99999, 100002])
+@pytest.mark.parametrize("pos", [0, 1, 2, 3, 4, 5, 1023, 1024, 2047, 2048, 2049, 4095, 4096, 4097, 6143, 50001, 99999, 100002])
 def test_rounding_event_mid_chunk(device, dt, pos):
     """An inexact add at `pos`.  Whether the candidates after it still verify
     depends on the data (a later rounding of the exact sum may or may not

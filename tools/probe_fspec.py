@@ -48,6 +48,9 @@ if __name__ == "__main__":
             out[f"serial_{dt}_16MiB_smooth"] = time_decode(dt, (16 << 20) // np.dtype(dt).itemsize, "smooth", reps=3)
         print(json.dumps(out))
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "prof":  # the smooth 256 MiB cases only (rocprofv3)
+        print(json.dumps({dt: time_decode(dt, (256 << 20) // np.dtype(dt).itemsize, "smooth") for dt in ("<f4", "<f8")}))
+        sys.exit(0)
     # the serial leg runs in a child started before this process touches the GPU
     r = subprocess.run([sys.executable, __file__, "serial"], capture_output=True, text=True, timeout=300)
     out = json.loads(r.stdout.strip().splitlines()[-1])
