@@ -143,6 +143,20 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
  * Decode runs one workgroup per chunk (integer: single-pass scan with a
  * running carry; float: one sequential add chain per chunk) and needs no
  * workspace. */
+/* mc_delta_decode_batch with a workspace (mc_delta_decode_batch_workspace
+ * bytes: 8 per chunk for f4/f8 with astype == dtype, else 0).  f4/f8 chunks
+ * (16-B aligned buffers and strides) then decode by the verified
+ * speculative scan of mc_delta_decode, one workgroup per chunk, and chunks
+ * with a rounding mismatch finish as a serial chain from the start of the
+ * 16 KiB tile holding it (bit-exact for any data); workspace[c] = that
+ * element index (n if the chunk verified entirely).  Every
+ * other case, or no workspace, is mc_delta_decode_batch. */
+size_t mc_delta_decode_batch_workspace(size_t nchunks, size_t n, int astype,
+                                       int dtype);
+int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst,
+                             size_t dst_stride, size_t nchunks, size_t n,
+                             int astype, int dtype, void *workspace,
+                             size_t workspace_bytes, mc_stream_t stream);
 int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst,
                           size_t dst_stride, size_t nchunks, size_t n,
                           int dtype, int astype, mc_stream_t stream);

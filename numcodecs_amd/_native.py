@@ -83,6 +83,9 @@ _SIGNATURES = {
     "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
     "mc_delta_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
+    "mc_delta_decode_batch_workspace": [_c_size, _c_size, _c_int, _c_int],
+    "mc_delta_decode_batch_ws": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp, _c_size,
+                                 _c_vp],
     "mc_delta_decode_batch_variant": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_int,
                                       _c_vp],
     "mc_fso_encode": [
@@ -139,6 +142,7 @@ _SIGNATURES = {
 _RESTYPES = {
     "mc_strerror": ctypes.c_char_p,
     "mc_delta_decode_workspace": ctypes.c_size_t,
+    "mc_delta_decode_batch_workspace": ctypes.c_size_t,
     "mc_fletcher32_workspace": ctypes.c_size_t,
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,

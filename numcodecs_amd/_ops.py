@@ -126,9 +126,12 @@ def delta_batch(src, src_stride, dst, dst_stride, nchunks, n, dtype, astype, enc
                                             dtype_code(dtype), dtype_code(astype), stream(src)),
                   "mc_delta_encode_batch")
         else:
-            check(lib.mc_delta_decode_batch(src.data_ptr(), src_stride, dst.data_ptr(), dst_stride, nchunks, n,
-                                            dtype_code(astype), dtype_code(dtype), stream(src)),
-                  "mc_delta_decode_batch")
+            a, d = dtype_code(astype), dtype_code(dtype)
+            ws_n = lib.mc_delta_decode_batch_workspace(nchunks, n, a, d)
+            ws = workspace(ws_n, src)
+            check(lib.mc_delta_decode_batch_ws(src.data_ptr(), src_stride, dst.data_ptr(), dst_stride, nchunks, n,
+                                               a, d, ws.data_ptr(), ws.numel(), stream(src)),
+                  "mc_delta_decode_batch_ws")
 
 
 def delta_decode(src, dst, n, astype, dtype) -> None:

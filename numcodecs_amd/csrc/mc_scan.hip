@@ -177,16 +177,18 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
   const int as = mc_itemsize(a);
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
-  // fix-up mode (single chunk, after k_fspec_apply): the chain restarts at
+  // fix-up mode (after k_fspec_apply / k_fspec_rows; startp[row]): the chain restarts at
   // the first element whose speculative value failed verification (rounded
-  // down to a multiple of 4 so vector accesses stay aligned), carrying the
+  // down to a 128-B boundary so vector accesses stay aligned), carrying the
   // verified value before it; nothing to do if every element verified
   bool has_carry = false;
   T carry = 0;
   if (startp) {
-    size_t s0 = (size_t)*startp;
+    size_t s0 = (size_t)startp[blockIdx.x];
     if (s0 >= n) return;
-    s0 &= ~(size_t)3;
+    // restart on a 128-B line of dst: the chain's block loads/stores stay
+    // line-aligned (a 16-B offset cost 15 % on 2048 x 1 MiB f4 rows)
+    s0 &= ~(size_t)(128 / DS - 1);
     if (s0 > 0) {
       has_carry = true;
       const uint64_t cb = mc_load_elem_u(dst, s0 - 1, DS);
@@ -974,6 +976,106 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   if (lane == 0 && first != ~(uint64_t)0) atomicMin((unsigned long long *)fail, (unsigned long long)first);
 }
 
+// Batched speculative float Delta decode: one workgroup per chunk walks it
+// in tiles with a running double prefix `carry` (the next tile's candidates
+// are carry + in-tile prefix, and its first element's predecessor is the
+// previous tile's last candidate), verifying every element as in
+// k_fspec_apply.  At the first tile with a failing element the workgroup
+// records the tile's start in fail[row] and stops without storing it;
+// k_scan_serial (fix-up mode, one chain per row) then finishes that row.
+// fail[row] = n when the whole row verified.
+template <typename T>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restrict__ src,
+                                                        size_t src_stride, uint8_t *__restrict__ dst,
+                                                        size_t dst_stride, size_t n,
+                                                        uint64_t *__restrict__ fail) {
+  constexpr int W = fs_w<T>();
+  typedef T vec __attribute__((ext_vector_type(W)));
+  __shared__ double lds[2][FS_Q][MC_BLOCK / 64];
+  __shared__ T ldsc[2][FS_Q][MC_BLOCK / 64];
+  __shared__ uint64_t ldsf[2][MC_BLOCK / 64];
+  __shared__ double ldsp[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  src += (size_t)blockIdx.x * src_stride;
+  dst += (size_t)blockIdx.x * dst_stride;
+  double carry = 0.0;
+  T prevc = (T)0;
+  int par = 0;
+  T nv[FS_Q][W];
+  fs_load<T>(src, n, 0, nv);
+  for (size_t t0 = 0; t0 < n; t0 += fs_tile<T>(), par ^= 1) {
+    T v[FS_Q][W];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q)
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
+    if (t0 + fs_tile<T>() < n) fs_load<T>(src, n, t0 + fs_tile<T>(), nv);  // next tile in flight
+    double p[FS_Q][W];
+    fs_tile_scan<T>(v, p, lds[par]);
+    T c[FS_Q][W], up[FS_Q];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+#pragma unroll
+      for (int e = 0; e < W; ++e) c[q][e] = (T)(carry + p[q][e]);
+      up[q] = __shfl_up(c[q][W - 1], 1, 64);
+      if (lane == 63) ldsc[par][q][wave] = c[q][W - 1];
+    }
+    __syncthreads();
+    uint64_t first = ~(uint64_t)0;
+#pragma unroll
+    for (int q = FS_Q - 1; q >= 0; --q) {
+      T p0;
+      if (lane) p0 = up[q];
+      else if (wave) p0 = ldsc[par][q][wave - 1];
+      else p0 = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
+      const size_t e0 = fs_elem0<T>(t0, q);
+#pragma unroll
+      for (int e = W - 1; e >= 0; --e) {
+        const size_t g = e0 + e;
+        const T pv = e ? c[q][e - 1] : p0;
+        const T r = g == 0 ? v[q][0] : (T)(pv + v[q][e]);
+        const bool ok = fs_bits<T>(c[q][e]) == fs_bits<T>(r) && __builtin_isfinite(c[q][e]);
+        if (g < n && !ok) first = g;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(first, off, 64);
+      first = o < first ? o : first;
+    }
+    if (lane == 0) ldsf[par][wave] = first;
+    if (threadIdx.x == MC_BLOCK - 1) ldsp[par] = carry + p[FS_Q - 1][W - 1];
+    __syncthreads();
+    uint64_t tf = ldsf[par][0];
+#pragma unroll
+    for (int j = 1; j < MC_BLOCK / 64; ++j) tf = ldsf[par][j] < tf ? ldsf[par][j] : tf;
+    if (tf != ~(uint64_t)0) {  // uniform across the workgroup
+      // the failing tile is not stored: the serial fix-up restarts at its
+      // first element (a chunk that fails in its first tile -- random data --
+      // then costs the serial chain alone, with no speculative stores)
+      if (threadIdx.x == 0) fail[blockIdx.x] = t0;
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const size_t e0 = fs_elem0<T>(t0, q);
+      if (e0 + W <= n) {
+        vec x;
+#pragma unroll
+        for (int e = 0; e < W; ++e) x[e] = c[q][e];
+        __builtin_nontemporal_store(x, reinterpret_cast<vec *>(dst + e0 * sizeof(T)));
+      } else {
+        for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<T *>(dst)[e0 + e] = c[q][e];
+      }
+    }
+    // next tile: prefix = this tile's last prefix (thread MC_BLOCK-1's, via
+    // LDS), predecessor = this tile's last candidate
+    carry = ldsp[par];
+    prevc = ldsc[par][FS_Q - 1][MC_BLOCK / 64 - 1];
+  }
+  if (threadIdx.x == 0) fail[blockIdx.x] = n;
+}
+
 // MCODEC_FSPEC=0 disables the speculative float path (A/B: serial only)
 static bool fspec_enabled() {
   static const bool b = [] {
@@ -1070,6 +1172,46 @@ int mc_delta_decode_batch(const void *src, size_t src_stride, void *dst, size_t 
                           size_t nchunks, size_t n, int astype, int dtype, mc_stream_t stream) {
   return mc_delta_decode_batch_variant(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype,
                                        0, stream);
+}
+
+size_t mc_delta_decode_batch_workspace(size_t nchunks, size_t n, int astype, int dtype) {
+  (void)n;
+  return astype == dtype && (dtype == MC_F4 || dtype == MC_F8) ? nchunks * sizeof(uint64_t) : 0;
+}
+
+int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                             size_t nchunks, size_t n, int astype, int dtype, void *workspace,
+                             size_t workspace_bytes, mc_stream_t stream) {
+  const bool spec = astype == dtype && (dtype == MC_F4 || dtype == MC_F8) && fspec_enabled() && workspace &&
+                    workspace_bytes >= nchunks * sizeof(uint64_t) && (uintptr_t)workspace % 8 == 0 &&
+                    (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
+                    (nchunks == 1 || (src_stride % 16 == 0 && dst_stride % 16 == 0));
+  if (!spec || n == 0 || nchunks == 0 || !src || !dst ||
+      (nchunks > 1 && (src_stride < n * mc_itemsize(astype) || dst_stride < n * mc_itemsize(dtype))))
+    return mc_delta_decode_batch(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype, stream);
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  uint64_t *fail = static_cast<uint64_t *>(workspace);
+  constexpr size_t GRID_MAX = 1u << 30;
+  for (size_t c0 = 0; c0 < nchunks; c0 += GRID_MAX) {
+    const unsigned g = (unsigned)min(GRID_MAX, nchunks - c0);
+    const uint8_t *sc = s + c0 * src_stride;
+    uint8_t *dc = d + c0 * dst_stride;
+    // rows that failed verification finish as one serial chain each (the
+    // schedules of launch_serial: small LDS slots when many chains share a
+    // CU; 4 KiB slots measured no different here)
+    if (dtype == MC_F8) {
+      k_fspec_rows<double><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, fail + c0);
+      if (g >= 256) k_scan_serial<MC_F8, MC_F8, true, 8192, 16><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
+      else k_scan_serial<MC_F8, MC_F8, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
+    } else {
+      k_fspec_rows<float><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, fail + c0);
+      if (g >= 256) k_scan_serial<MC_F4, MC_F4, true, 8192, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
+      else k_scan_serial<MC_F4, MC_F4, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
+    }
+  }
+  return mc_last_launch();
 }
 
 int mc_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst,

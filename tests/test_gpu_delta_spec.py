@@ -159,3 +159,65 @@ def test_repeated_calls_reset_failure_word(device, dt):
                                                   _ops.stream(src)), "mc_delta_decode")
         assert dst.cpu().numpy().tobytes() == _oracle_dec(enc, dt).tobytes()
         assert int(ws[-1].item()) == (n if enc is good else 7)
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("n,pad", [(1, 0), (2047, 16), (4096, 0), (10007, 48), (70001, 0), (1001, -1)])
+def test_batch_rows_mixed(device, dt, n, pad):
+    """mc_delta_decode_batch_ws: smooth rows verify entirely (workspace[row] =
+    n), rows with rounding or non-finite values finish serially; every row
+    equals numpy's cumsum of that row."""
+    dev = torch.device("cuda", 0)
+    it = np.dtype(dt).itemsize
+    rows = 37
+    # 16-B aligned row strides take the speculative path; pad = -1 gives an
+    # unaligned stride, which takes the serial batch path (output only checked)
+    stride = n * it + 4 if pad < 0 else -(-n * it // 16) * 16 + pad
+    spec = pad >= 0
+    raw = np.zeros((rows, stride), dtype=np.uint8)
+    encs, smooth = [], []
+    for r in range(rows):
+        kind = ("ramp", "sine", "ints", "random", "inf")[r % 5]
+        if kind == "random":
+            enc = RNG.normal(0, 1, n).astype(dt)
+        else:
+            enc = _oracle_enc(_smooth(dt, n, "ints" if kind == "inf" else kind), dt)
+            if kind == "inf":
+                enc[(r * 7919) % n] = np.inf
+        encs.append(enc)
+        smooth.append(kind in ("ramp", "sine", "ints"))
+        raw[r, : n * it] = enc.view(np.uint8)
+    src = torch.from_numpy(raw).to(dev)
+    dst = torch.zeros_like(src)
+    a = _ops.dtype_code(dt)
+    ws_n = _native.lib.mc_delta_decode_batch_workspace(rows, n, a, a)
+    assert ws_n == 8 * rows
+    ws = torch.zeros(rows, dtype=torch.int64, device=dev)
+    _native.check(_native.lib.mc_delta_decode_batch_ws(src.data_ptr(), stride, dst.data_ptr(), stride, rows, n,
+                                                       a, a, ws.data_ptr(), ws_n, _ops.stream(src)),
+                  "mc_delta_decode_batch_ws")
+    got = dst.cpu().numpy()
+    fails = ws.cpu().numpy()
+    for r in range(rows):
+        ref = _oracle_dec(encs[r], dt)
+        assert got[r, : n * it].tobytes() == ref.tobytes(), r
+        assert not got[r, n * it:].any()  # padding untouched
+        if not spec:
+            assert fails[r] == 0  # workspace untouched
+        elif smooth[r]:
+            assert fails[r] == n, (r, fails[r])
+        elif n > 2:
+            assert fails[r] < n, (r, fails[r])
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+def test_batch_api_smooth_chunks(device, dt):
+    """batch.delta_chunks decode (the batched codec path) on smooth chunks."""
+    from numcodecs_amd import batch
+
+    n = 1 << 16
+    xs = np.stack([_smooth(dt, n, "sine") + np.asarray(k, dtype=dt) for k in range(24)])
+    xd = torch.from_numpy(xs).to(device)
+    enc = batch.delta_chunks(xd, Delta(dt), encode=True)
+    dec = batch.delta_chunks(enc, Delta(dt), encode=False)
+    assert dec.cpu().numpy().tobytes() == xs.tobytes()
