@@ -919,7 +919,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t tile = blockIdx.x;
   const size_t t0 = tile * fs_tile<T>();
-  // a tile at or past a recorded failure is recomputed by the serial fix-up
+  // a tile at or past a recorded failure is recomputed by the serial fix-up.
+  // Each wave reads the word itself, so waves of one workgroup may disagree
+  // when another tile's atomicMin lands in between: the exited waves leave
+  // the barriers (s_barrier waits for surviving waves only) and the
+  // remaining ones compute garbage for this tile -- harmless, because the
+  // whole tile lies at or past a recorded failure, so the fix-up rewrites
+  // it, and any index these waves report is >= t0, above the minimum.
   if (__builtin_nontemporal_load(fail) <= t0) return;
   T v[FS_Q][W];
   fs_load<T>(src, n, t0, v);
