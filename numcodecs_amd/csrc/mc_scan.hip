@@ -732,7 +732,7 @@ static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, h
 //   1. k_fspec_reduce: per-tile total of the tile's prefix sums in double,
 //      with the same block-scan code as the apply pass, so a tile's total is
 //      bitwise the value its last element's candidate is built from;
-//   2. k_fspec_sums: exclusive scan of the totals (any order: each tile only
+//   2. k_fspec_pre: exclusive scan of the totals (any order: each tile only
 //      uses its own prefix and its predecessor's) and reset of the
 //      first-failure word;
 //   3. k_fspec_apply: candidate c_i = dtype(S_tile + local prefix_i); every
@@ -843,67 +843,6 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__rest
   double p[FS_Q][W];
   fs_tile_scan<T>(v, p, lds);
   if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = p[FS_Q - 1][W - 1];
-}
-
-// exclusive scan of the tile totals by one workgroup, in rounds of
-// 1024 x FS_SR totals staged through LDS: coalesced loads into LDS, each
-// thread scans FS_SR consecutive totals in registers, one wave scan of the
-// thread totals and one LDS exchange of the wave totals, prefixes written
-// back through LDS and stored coalesced.  (Scanning 64 values per wave step
-// instead costs 16x more cross-lane shuffles, all through one CU's LDS
-// crossbar: 16 us for 16 Ki tiles.)  Also sets the first-failure word := n.
-constexpr int FS_SR = 4;
-__global__ __launch_bounds__(1024) void k_fspec_sums(const double *__restrict__ sums,
-                                                     double *__restrict__ pre, size_t ntiles,
-                                                     uint64_t *__restrict__ fail, size_t n) {
-  __shared__ double stage[1024 * FS_SR];
-  __shared__ double lds[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double carry = 0.0;
-  for (size_t r0 = 0; r0 < ntiles; r0 += (size_t)1024 * FS_SR) {
-#pragma unroll
-    for (int k = 0; k < FS_SR; ++k) {
-      const size_t i = r0 + (size_t)k * 1024 + threadIdx.x;
-      stage[k * 1024 + threadIdx.x] = i < ntiles ? sums[i] : 0.0;
-    }
-    __syncthreads();
-    double x[FS_SR];
-#pragma unroll
-    for (int k = 0; k < FS_SR; ++k) x[k] = stage[threadIdx.x * FS_SR + k];
-    double r = x[0];
-#pragma unroll
-    for (int k = 1; k < FS_SR; ++k) r += x[k];
-    double incl = r;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double o = __shfl_up(incl, off, 64);
-      if (lane >= off) incl = o + incl;
-    }
-    if (lane == 63) lds[wave] = incl;
-    const double ex = __shfl_up(incl, 1, 64);
-    __syncthreads();
-    double run = carry, tot = 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (j < wave) run += lds[j];
-      tot += lds[j];
-    }
-    if (lane) run += ex;
-#pragma unroll
-    for (int k = 0; k < FS_SR; ++k) {
-      stage[threadIdx.x * FS_SR + k] = run;
-      run += x[k];
-    }
-    carry += tot;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FS_SR; ++k) {
-      const size_t i = r0 + (size_t)k * 1024 + threadIdx.x;
-      if (i < ntiles) pre[i] = stage[k * 1024 + threadIdx.x];
-    }
-    __syncthreads();  // stage and lds reused by the next round
-  }
-  if (threadIdx.x == 0) *fail = n;
 }
 
 template <typename T>
@@ -1099,6 +1038,50 @@ static size_t fspec_ntiles(size_t n, int dt) {
 // tile totals, tile prefixes, the failure word
 static size_t fspec_ws_bytes(size_t n, int dt) { return (2 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
 
+// Tile prefixes by many workgroups (one per 256 tiles): workgroup g sums
+// all totals before its range itself (coalesced, 8 loads in flight per
+// thread) and scans its own 256.  A one-workgroup scan (LDS-staged, 4096
+// totals per round) was bound by a single CU's bandwidth: 14.7 us for
+// 16 Ki tiles against 7.9 us here; reading the earlier totals redundantly
+// spreads that over ntiles/256 CUs.  Any association is
+// fine: the apply pass only relies on the stored pre[] and sums[].
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict__ sums,
+                                                       double *__restrict__ pre, size_t ntiles,
+                                                       uint64_t *__restrict__ fail, size_t n) {
+  __shared__ double lds[2][MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t b = (size_t)blockIdx.x * MC_BLOCK;
+  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t i = threadIdx.x;
+  for (; i + 7 * MC_BLOCK < b; i += 8 * MC_BLOCK) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += sums[i + (size_t)k * MC_BLOCK];
+  }
+  for (; i < b; i += MC_BLOCK) a[0] += sums[i];
+  double acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  const double x = b + threadIdx.x < ntiles ? sums[b + threadIdx.x] : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  double incl = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl = o + incl;
+  }
+  const double ex = __shfl_up(incl, 1, 64);
+  if (lane == 0) lds[0][wave] = acc;
+  if (lane == 63) lds[1][wave] = incl;
+  __syncthreads();
+  double base = 0.0, w = 0.0;
+#pragma unroll
+  for (int j = 0; j < MC_BLOCK / 64; ++j) {
+    base += lds[0][j];
+    if (j < wave) w += lds[1][j];
+  }
+  if (b + threadIdx.x < ntiles) pre[b + threadIdx.x] = base + (w + (lane ? ex : 0.0));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *fail = n;
+}
+
 template <int D>
 static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipStream_t st) {
   using T = typename std::conditional<D == MC_F8, double, float>::type;
@@ -1106,7 +1089,7 @@ static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipSt
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
   uint64_t *fail = reinterpret_cast<uint64_t *>(pre + ntiles);
   k_fspec_reduce<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, sums);
-  k_fspec_sums<<<1, 1024, 0, st>>>(sums, pre, ntiles, fail, n);
+  k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, fail, n);
   k_fspec_apply<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, sums, pre, fail);
   k_scan_serial<D, D, true, 32768, 32><<<1, 128, 0, st>>>(s, 0, d, 0, n, D, fail);
 }
