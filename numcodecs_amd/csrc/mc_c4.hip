@@ -469,11 +469,11 @@ template <int D, int A>
 static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Params &p,
                       hipStream_t st) {
   const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  const size_t npairs = (ntiles + 1) / 2;  // workspace: 16 + 8 * ntiles >= 16 * npairs
-  uint64_t *pair = sums, *first = sums + npairs;
+  const size_t npairs = (ntiles + 1) / 2;  // workspace: 3 * 8 * npairs bytes
+  uint64_t *pair = sums, *first = sums + npairs, *pre = sums + 2 * npairs;
   k_c4_reduce2<D, A><<<(unsigned)npairs, MC_BLOCK, 0, st>>>(s, pair, first, p);
-  mc_launch_scan_sums<false>(pair, npairs, st);
-  k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, pair, first, p);
+  mc_launch_scan_sums_mw<false>(pair, pre, npairs, st);
+  k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, pre, first, p);
 }
 
 // MCODEC_C4_VARIANT: 2 = single-pass look-back decode with an atomic tile
@@ -541,7 +541,8 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
 
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n) {
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  return mc_lb_workspace(ntiles) > ntiles * 8 ? mc_lb_workspace(ntiles) : ntiles * 8;
+  const size_t scan3 = 24 * ((ntiles + 1) / 2);  // pair totals, first values, pair prefixes
+  return mc_lb_workspace(ntiles) > scan3 ? mc_lb_workspace(ntiles) : scan3;
 }
 
 int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n, int astype, int dtype,

@@ -146,6 +146,46 @@ static inline void mc_launch_scan_sums(uint64_t *sums, size_t ntiles, hipStream_
   k_scan_sums<OR_OP><<<1, 1024, 0, st>>>(sums, ntiles);
 }
 
+// Exclusive scan of n totals into a separate array by one workgroup per 256
+// totals: workgroup g combines every total before its range itself
+// (coalesced, 8 loads in flight per thread) and scans its own 256.  The
+// one-workgroup k_scan_sums is bound by a single CU (4.8 us for one round of
+// 8192, ~8 us in the C4 decode); reading the earlier totals redundantly
+// spreads the work over n/256 CUs.  Not in place (in != out).
+template <bool OR_OP>
+__global__ __launch_bounds__(MC_BLOCK) void k_scan_sums_mw(const uint64_t *__restrict__ in,
+                                                          uint64_t *__restrict__ out, size_t n) {
+  __shared__ uint64_t red[MC_BLOCK / 64];
+  __shared__ uint64_t base_lds[MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t b = (size_t)blockIdx.x * MC_BLOCK;
+  uint64_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t i = threadIdx.x;
+  for (; i + 7 * MC_BLOCK < b; i += 8 * MC_BLOCK) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = mc_scan_combine<OR_OP>(a[k], in[i + (size_t)k * MC_BLOCK]);
+  }
+  for (; i < b; i += MC_BLOCK) a[0] = mc_scan_combine<OR_OP>(a[0], in[i]);
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc = mc_scan_combine<OR_OP>(acc, a[k]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = mc_scan_combine<OR_OP>(acc, __shfl_xor(acc, off, 64));
+  if (lane == 0) base_lds[wave] = acc;
+  const uint64_t x = b + threadIdx.x < n ? in[b + threadIdx.x] : 0;
+  uint64_t tot;
+  const uint64_t ex = mc_block_excl_scan<OR_OP>(x, red, &tot);  // its barriers publish base_lds
+  uint64_t base = 0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) base = mc_scan_combine<OR_OP>(base, base_lds[w]);
+  if (b + threadIdx.x < n) out[b + threadIdx.x] = mc_scan_combine<OR_OP>(base, ex);
+}
+
+template <bool OR_OP>
+static inline void mc_launch_scan_sums_mw(const uint64_t *in, uint64_t *out, size_t n, hipStream_t st) {
+  k_scan_sums_mw<OR_OP><<<(unsigned)((n + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(in, out, n);
+}
+
 // ---------------------------------------------------------------------------
 // Decoupled look-back (single-pass scan across workgroups).
 //

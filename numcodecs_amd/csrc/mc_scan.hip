@@ -643,11 +643,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply(const uint8_t *__restr
   ds_store_half<ES>(dst, n, eb0, v, H);
 }
 
-// workspace entries of the fast path: part[] (whole groups of tiles) + group sums
+// workspace entries of the fast path: group sums, part[] (whole groups of
+// tiles), group prefixes
 static size_t dscan_ws_entries(size_t n, int es) {
   const size_t te = (size_t)(32 / es) * MC_BLOCK;
   const size_t ngroups = ((n + te - 1) / te + DS_GROUP - 1) / DS_GROUP;
-  return ngroups * DS_GROUP + ngroups;
+  return ngroups * DS_GROUP + 2 * ngroups;
 }
 
 // Batched same-width integer Delta decode: one workgroup per chunk walks it in
@@ -714,10 +715,10 @@ template <int ES>
 static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, hipStream_t st) {
   const size_t ntiles = (n + ds_tile<ES>() - 1) / ds_tile<ES>();
   const size_t ngroups = (ntiles + DS_GROUP - 1) / DS_GROUP;
-  uint64_t *group = ws, *part = ws + ngroups;
+  uint64_t *group = ws, *part = ws + ngroups, *gpre = part + DS_GROUP * ngroups;
   k_dscan_reduce<ES><<<(unsigned)ngroups, MC_BLOCK, 0, st>>>(s, n, group, part);
-  mc_launch_scan_sums<false>(group, ngroups, st);
-  k_dscan_apply<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, group, part);
+  mc_launch_scan_sums_mw<false>(group, gpre, ngroups, st);
+  k_dscan_apply<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, gpre, part);
 }
 
 
