@@ -339,33 +339,6 @@ enum mc_blosc_mode { MC_BLOSC_NOSHUFFLE = 0, MC_BLOSC_SHUFFLE = 1, MC_BLOSC_BITS
 int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize,
                     size_t blocksize, int mode, int forward, mc_stream_t stream);
 
-/* ---- tuning / measurement hooks (bench.py) ----------------------------- */
-/* mc_fso_delta_shuffle_decode with an explicit decode schedule: 0 default,
- * 1 three-pass scan, 2 single-pass look-back with an atomic tile counter,
- * 3 single-pass look-back in workgroup order, 4 = 3 with every wait replaced
- * by the data-derived prefix fallback (for tests), 5 / 6 single-pass
- * look-back over partitions of 4 / 8 tiles held in registers, 7 = 5 with
- * the forced fallback (for tests).  All give identical bytes. */
-int mc_fso_delta_shuffle_decode_variant(const void *src, void *dst, size_t n,
-                                        int astype, int dtype, double scale,
-                                        double offset, void *workspace,
-                                        size_t workspace_bytes, int variant,
-                                        mc_stream_t stream);
-/* mc_delta_decode_batch with an explicit float-chain schedule (LDS slot
- * bytes / chain values per LDS read group): 0 default (by batch size),
- * 1 32 KiB/16, 2 32 KiB/32, 3 8 KiB/16, 4 8 KiB/32, 5 4 KiB/32.  Integer
- * dtypes ignore it.  All give identical bytes. */
-int mc_delta_decode_batch_variant(const void *src, size_t src_stride,
-                                  void *dst, size_t dst_stride,
-                                  size_t nchunks, size_t n, int astype,
-                                  int dtype, int variant, mc_stream_t stream);
-/* Shuffle with an explicit kernel variant and grid (0 = default); used by
- * bench.py to sweep variants.  variant: 0 default, 1 register/dword stores,
- * 2 LDS-staged 16-B stores, 3 LDS both sides, 4 generic byte kernel. */
-int mc_shuffle_variant(const void *src, void *dst, size_t nbytes,
-                       size_t elementsize, int encode, int variant,
-                       int max_blocks, mc_stream_t stream);
-
 #ifdef __cplusplus
 }
 #endif

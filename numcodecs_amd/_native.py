@@ -86,8 +86,6 @@ _SIGNATURES = {
     "mc_delta_decode_batch_workspace": [_c_size, _c_size, _c_int, _c_int],
     "mc_delta_decode_batch_ws": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp, _c_size,
                                  _c_vp],
-    "mc_delta_decode_batch_variant": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_int,
-                                      _c_vp],
     "mc_fso_encode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int,
         _c_double, _c_i64, _c_double, _c_i64, _c_vp,
@@ -116,10 +114,6 @@ _SIGNATURES = {
     "mc_fso_delta_shuffle_decode_workspace": [_c_size],
     "mc_fso_delta_shuffle_decode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
-    ],
-    "mc_shuffle_variant": [_c_vp, _c_vp, _c_size, _c_size, _c_int, _c_int, _c_int, _c_vp],
-    "mc_fso_delta_shuffle_decode_variant": [
-        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_int, _c_vp,
     ],
     "mc_checksum32_workspace": [_c_int, _c_size, _c_size],
     "mc_checksum32_batch": [

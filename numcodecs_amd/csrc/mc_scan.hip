@@ -1097,6 +1097,10 @@ static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipSt
 
 }  // namespace
 
+int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                               size_t nchunks, size_t n, int astype, int dtype, int variant,
+                               mc_stream_t stream);
+
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
@@ -1160,8 +1164,8 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
 
 int mc_delta_decode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
                           size_t nchunks, size_t n, int astype, int dtype, mc_stream_t stream) {
-  return mc_delta_decode_batch_variant(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype,
-                                       0, stream);
+  return mc_delta_decode_batch_impl(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype, 0,
+                                    stream);
 }
 
 size_t mc_delta_decode_batch_workspace(size_t nchunks, size_t n, int astype, int dtype) {
@@ -1204,9 +1208,14 @@ int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst, size
   return mc_last_launch();
 }
 
-int mc_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst,
-                                  size_t dst_stride, size_t nchunks, size_t n, int astype,
-                                  int dtype, int variant, mc_stream_t stream) {
+}  // extern "C"
+
+// Batched Delta decode with an explicit float-chain schedule (0 = default by
+// batch size; 1-5 the LDS slot / read-group sweep of tools/lab).  C++
+// linkage: the C ABI exposes the default only (mc_delta_decode_batch).
+int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                               size_t nchunks, size_t n, int astype, int dtype, int variant,
+                               mc_stream_t stream) {
   if (variant < 0 || variant > 5) return MC_EINVAL;
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
   if (n == 0 || nchunks == 0) return MC_OK;
@@ -1255,5 +1264,3 @@ int mc_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst,
   }
   return mc_last_launch();
 }
-
-}  // extern "C"

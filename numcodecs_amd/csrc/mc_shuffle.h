@@ -55,3 +55,10 @@ MC_DEV void store_quad(uint8_t *p, const uint32_t (&w)[ES]) {
   }
 }
 
+// Shared driver of every shuffle entry point (mc_shuffle.hip), also used by
+// the fused Shuffle+Fletcher32 ops: variant 0 = the measured default schedule
+// (the other layouts exist for the lab's sweeps, tools/lab); br != NULL fuses
+// BitRound into the encode.
+int mc_shuffle_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride, size_t nchunks,
+                    size_t chunk_bytes, size_t es, bool enc, int variant, int max_blocks, const McBitRound *br,
+                    hipStream_t st);

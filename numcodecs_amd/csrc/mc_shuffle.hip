@@ -739,15 +739,6 @@ int mc_unshuffle_batch(const void *src, size_t src_stride, void *dst, size_t dst
                          elementsize, false, V_DEFAULT, 0, nullptr, (hipStream_t)stream);
 }
 
-int mc_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize,
-                       int encode, int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > V_PAIR ||
-      (variant & ~(7 | V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE)) != 0)
-    return MC_EINVAL;
-  return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant,
-                         max_blocks, nullptr, (hipStream_t)stream);
-}
-
 int mc_bitround_shuffle(const void *src, void *dst, size_t n, int itemsize, int keepbits,
                         mc_stream_t stream) {
   if (!(itemsize == 2 || itemsize == 4 || itemsize == 8)) return MC_EINVAL;

@@ -69,7 +69,16 @@ class Fletcher32(Codec):
             if is_device_tensor(out):
                 out_flat = ensure_contiguous_ndarray(out)
                 out_raw = out_flat.view(torch.uint8) if out_flat.numel() else out_flat.new_empty(0, dtype=torch.uint8)
-                _ops.copy(payload, out_raw, payload.numel())
+                # the reference memcpys into `out` unchecked (fletcher32.pyx:107-111);
+                # an undersized device buffer must not become an out-of-bounds write
+                if out_raw.numel() < payload.numel():
+                    raise ValueError(
+                        f"cannot copy {payload.numel()} bytes into an output buffer of {out_raw.numel()} bytes"
+                    )
+                if out_raw.device != payload.device:
+                    out_raw[: payload.numel()].copy_(payload)
+                else:
+                    _ops.copy(payload, out_raw, payload.numel())
                 return out
             o = ensure_contiguous_ndarray(out).view("uint8")
             o[: payload.numel()] = download(payload)

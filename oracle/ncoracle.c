@@ -18,6 +18,7 @@
  * Built with plain -O3 and no -march, like the reference's release build
  * (src/numcodecs/meson.build:245-254).
  */
+#include <math.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -75,6 +76,70 @@ void nco_unshuffle_batch(const uint8_t *src, uint8_t *des, size_t nchunks, size_
                          size_t element_size) {
   for (size_t c = 0; c < nchunks; c++)
     nco_unshuffle(src + c * chunk_bytes, des + c * chunk_bytes, chunk_bytes, element_size);
+}
+
+/* ---- numpy-semantics elementwise codecs (CPU baseline of C3/C4) ---------
+ * The reference expresses these in numpy; restated here as scalar C loops
+ * with numpy's numerics (checked bit-exact against tests/golden by
+ * tests/test_oracle.py::test_c_restatement_*).  Each call is ONE pass, where
+ * numpy makes several (BitRound: copy + 5 in-place ufunc passes; FSO: three
+ * temporaries + cast), so these loops are a faster CPU than the reference's
+ * own numpy path -- a conservative baseline. */
+
+/* bitround.py:62-68 on the int32 view of float32 data:
+ *   maskbits = 23 - keepbits; mask = -1 << maskbits (int32, wraps)
+ *   b += ((b >> maskbits) & 1) + ((1 << (maskbits - 1)) - 1); b &= mask
+ * numpy int32 arithmetic wraps: done in uint32.  0 <= keepbits < 23. */
+void nco_bitround32(const uint32_t *src, uint32_t *dst, size_t n, int keepbits) {
+  const unsigned maskbits = 23u - (unsigned)keepbits;
+  const uint32_t mask = 0xFFFFFFFFu << maskbits;
+  const uint32_t half = (1u << (maskbits - 1)) - 1u;
+  for (size_t i = 0; i < n; i++) {
+    uint32_t b = src[i];
+    b += ((b >> maskbits) & 1u) + half;
+    dst[i] = b & mask;
+  }
+}
+
+/* numpy's float -> int32 cast on x86-64 (cvttss2si): NaN and out-of-range
+ * values give INT32_MIN (the "integer indefinite"); int16 then truncates. */
+static int32_t nco_cvtt_f32(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)v;
+}
+
+/* fixedscaleoffset.py:91-97 with dtype '<f4', astype '<i2':
+ *   enc = np.around((arr - offset) * scale).astype('<i2')
+ * NEP 50: the Python scalars are weak, so both operations run in float32
+ * with offset/scale rounded to float32 (the caller passes them so). */
+void nco_fso_encode_f4_i2(const float *x, int16_t *out, size_t n, float offset, float scale) {
+  for (size_t i = 0; i < n; i++) {
+    const float v = rintf((x[i] - offset) * scale);
+    out[i] = (int16_t)nco_cvtt_f32(v);
+  }
+}
+
+/* fixedscaleoffset.py:107-110: dec = (enc / scale) + offset in float64
+ * (int16 array / Python float promotes to float64), then astype('<f4'). */
+void nco_fso_decode_i2_f4(const int16_t *enc, float *out, size_t n, double scale, double offset) {
+  for (size_t i = 0; i < n; i++) out[i] = (float)(((double)enc[i] / scale) + offset);
+}
+
+/* delta.py:63-66 with dtype = astype = '<i2': enc[0] = x[0]; enc[1:] = np.diff(x)
+ * (int16 subtraction wraps). */
+void nco_delta_encode_i2(const int16_t *x, int16_t *out, size_t n) {
+  if (n == 0) return;
+  out[0] = x[0];
+  for (size_t i = 1; i < n; i++) out[i] = (int16_t)(uint16_t)((uint16_t)x[i] - (uint16_t)x[i - 1]);
+}
+
+/* delta.py:80: np.cumsum(enc, out=dec) accumulated in int16 (wraps). */
+void nco_delta_decode_i2(const int16_t *enc, int16_t *out, size_t n) {
+  uint16_t run = 0;
+  for (size_t i = 0; i < n; i++) {
+    run = (uint16_t)(run + (uint16_t)enc[i]);
+    out[i] = (int16_t)run;
+  }
 }
 
 /* ---- jenkins.pyx:93-325 ------------------------------------------------ */

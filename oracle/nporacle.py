@@ -37,6 +37,11 @@ def _c():
         lib.nco_jenkins_lookup3.restype = ctypes.c_uint32
         lib.nco_crc32c.argtypes = [vp, sz, ctypes.c_uint32]
         lib.nco_crc32c.restype = ctypes.c_uint32
+        lib.nco_bitround32.argtypes = [vp, vp, sz, ctypes.c_int]
+        lib.nco_fso_encode_f4_i2.argtypes = [vp, vp, sz, ctypes.c_float, ctypes.c_float]
+        lib.nco_fso_decode_i2_f4.argtypes = [vp, vp, sz, ctypes.c_double, ctypes.c_double]
+        lib.nco_delta_encode_i2.argtypes = [vp, vp, sz]
+        lib.nco_delta_decode_i2.argtypes = [vp, vp, sz]
         _lib = lib
     return _lib
 
@@ -320,3 +325,38 @@ def shuffle_into(src: np.ndarray, dst: np.ndarray, elementsize: int) -> None:
 
 def unshuffle_into(src: np.ndarray, dst: np.ndarray, elementsize: int) -> None:
     _c().nco_unshuffle(_ptr(src), _ptr(dst), src.nbytes, elementsize)
+
+
+# C restatements of the numpy-expressed codecs (ncoracle.c), into caller
+# buffers; pinned bit-exact against the numpy restatements above and the
+# goldens by tests/test_oracle.py.
+def c_bitround32_into(src: np.ndarray, dst: np.ndarray, keepbits: int) -> None:
+    """bitround.py:62-68, float32 (0 <= keepbits < 23)."""
+    _c().nco_bitround32(_ptr(src), _ptr(dst), src.nbytes // 4, keepbits)
+
+
+def c_fso_encode_f4_i2_into(src: np.ndarray, dst: np.ndarray, offset, scale) -> None:
+    """fixedscaleoffset.py:91-97, '<f4' -> '<i2' (NEP 50: float32 compute,
+    offset/scale rounded to float32)."""
+    _c().nco_fso_encode_f4_i2(_ptr(src), _ptr(dst), src.nbytes // 4, float(np.float32(offset)),
+                              float(np.float32(scale)))
+
+
+def c_fso_decode_i2_f4_into(src: np.ndarray, dst: np.ndarray, offset, scale) -> None:
+    """fixedscaleoffset.py:107-110, '<i2' -> '<f4' through float64."""
+    _c().nco_fso_decode_i2_f4(_ptr(src), _ptr(dst), src.nbytes // 2, float(scale), float(offset))
+
+
+def c_delta_encode_i2_into(src: np.ndarray, dst: np.ndarray) -> None:
+    """delta.py:63-66, '<i2'."""
+    _c().nco_delta_encode_i2(_ptr(src), _ptr(dst), src.nbytes // 2)
+
+
+def c_delta_decode_i2_into(src: np.ndarray, dst: np.ndarray) -> None:
+    """delta.py:80 (np.cumsum in int16), '<i2'."""
+    _c().nco_delta_decode_i2(_ptr(src), _ptr(dst), src.nbytes // 2)
+
+
+def c_fletcher32(src: np.ndarray) -> int:
+    """fletcher32.pyx:24-57 over a contiguous uint8 array."""
+    return int(_c().nco_fletcher32(_ptr(src), src.nbytes))

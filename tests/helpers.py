@@ -91,3 +91,16 @@ def load_vectors():
 
 def vec(data, family, i, key):
     return data[f"{family}__{i}__{key}"]
+
+
+def lab_lib():
+    """libmcodec_lab.so (tools/lab): the product objects plus the measured and
+    rejected alternative schedules, which these tests keep byte-identical."""
+    import sys
+
+    tools = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    from lab.lablib import lab
+
+    return lab()

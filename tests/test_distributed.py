@@ -69,3 +69,37 @@ def test_chunk_range_and_aggregate():
     with pytest.raises(ValueError):
         chunk_range(10, 2, 2)
     assert aggregate_gibps(8 * (1 << 30), 2.0) == 4.0
+
+
+def test_bench_self_launches_ranks_dry_run():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself
+    (torch.distributed env set per child, gloo here: --dry-run touches no
+    GPU); their contiguous ranges cover all 8192 C5 chunks exactly once and
+    every rank round-trips a sample of its chunks through the oracle."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_ranks"] == 2 and d["chunks"] == 8192 and d["covered_all"]
+    assert [x["range"] for x in d["ranks"]] == [[0, 4096], [4096, 8192]]
+    assert len({x["pid"] for x in d["ranks"]}) == 2 and os.getpid() not in {x["pid"] for x in d["ranks"]}
+    assert all(x["ok"] for x in d["ranks"]) and d["max_over_ranks"] == 1.0
+
+
+def test_bench_world_size_mismatch_fails_loudly():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr

@@ -14,6 +14,7 @@ import torch
 import inputs
 import oracle
 from numcodecs_amd import Delta, FixedScaleOffset, Shuffle, batch
+from tests.helpers import lab_lib
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -98,9 +99,10 @@ def test_decode_schedules_identical(device, variant, dt, at):
     _, _, sc3, off4 = batch._c4_scalars(*codecs)
     raw = enc.view(torch.uint8).reshape(-1)
     out = torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, device=device)
-    ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_workspace(n), raw)
+    lab = lab_lib()
+    ws = _ops.workspace(lab.mc_lab_c4_decode_workspace(n), raw)
     for _ in range(2):  # a second call reuses the workspace: status words reset
-        check(lib.mc_fso_delta_shuffle_decode_variant(
+        check(lab.mc_lab_c4_decode_variant(
             raw.data_ptr(), out.data_ptr(), n, _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype),
             sc3, off4, ws.data_ptr(), ws.numel(), variant, _ops.stream(raw)), "decode_variant")
         assert torch.equal(out, ref.view(torch.uint8).reshape(-1)), variant

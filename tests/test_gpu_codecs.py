@@ -384,6 +384,23 @@ def test_fletcher32_out(device):
     assert f.decode(result, out=data) is data
 
 
+def test_fletcher32_device_out_sizes(device):
+    """Device `out`: exact and larger buffers receive the payload; an
+    undersized one raises ValueError instead of writing out of bounds (the
+    reference memcpys unchecked, fletcher32.pyx:107-111)."""
+    x = torch.randint(0, 256, (4099,), dtype=torch.uint8, device=device)
+    enc = Fletcher32().encode(x)
+    exact = torch.empty(4099, dtype=torch.uint8, device=device)
+    assert Fletcher32().decode(enc, out=exact) is exact and torch.equal(exact, x)
+    big = torch.zeros(5000, dtype=torch.uint8, device=device)
+    Fletcher32().decode(enc, out=big)
+    assert torch.equal(big[:4099], x) and not big[4099:].any()
+    small = torch.zeros(4098, dtype=torch.uint8, device=device)
+    with pytest.raises(ValueError):
+        Fletcher32().decode(enc, out=small)
+    assert not small.any()
+
+
 def test_fletcher32_vectors(device):
     for i, m in enumerate(MANIFEST["fletcher32"]):
         x = vec(DATA, "fletcher32", i, "input")

@@ -9,7 +9,7 @@ import torch
 
 import oracle
 from numcodecs_amd import BitRound, Shuffle, batch
-from numcodecs_amd._native import lib
+from tests.helpers import lab_lib
 
 pytestmark = pytest.mark.gpu
 RNG = np.random.default_rng(2024)
@@ -38,6 +38,7 @@ def test_shuffle_every_variant(device, es):
     big tiles, grouped and pipelined schedules, nt on/off) on sizes with and
     without a tail, through the tuning entry point."""
     st = torch.cuda.current_stream().cuda_stream
+    lib = lab_lib()
     variants = [1, 2, 3, 4, 9, 10, 11, 17, 129, 33, 65, 257, 273, 385, 5, 21, 133]
     for count in (4096 * 16 + 64, 16384 * 8, 4096 * 3 + 4):
         n = es * count
@@ -49,8 +50,8 @@ def test_shuffle_every_variant(device, es):
             for grid in (0, 7, 100000):
                 y = torch.empty_like(x)
                 z = torch.empty_like(x)
-                assert lib.mc_shuffle_variant(x.data_ptr(), y.data_ptr(), n, es, 1, v, grid, st) == 0
-                assert lib.mc_shuffle_variant(y.data_ptr(), z.data_ptr(), n, es, 0, v, grid, st) == 0
+                assert lib.mc_lab_shuffle_variant(x.data_ptr(), y.data_ptr(), n, es, 1, v, grid, st) == 0
+                assert lib.mc_lab_shuffle_variant(y.data_ptr(), z.data_ptr(), n, es, 0, v, grid, st) == 0
                 assert np.array_equal(y.cpu().numpy(), ref), (es, count, v, grid)
                 assert torch.equal(z, x), (es, count, v, grid)
 

@@ -249,14 +249,120 @@ def test_oracle_matches_reference_random():
         assert np.array_equal(oracle.bitround_encode(x.copy(), k), nc.BitRound(k).encode(x.copy()))
 
 
-def test_reference_cpu_baseline_importable():
-    """oracle/_ref's Cython _doShuffle is what bench.py times as the
-    cpu_baseline "reference" leg."""
+def test_port_equals_reference_cython_loops():
+    """bench.py's cpu_baseline times the C restatement (oracle/ncoracle.c),
+    never the reference; here (where oracle/_ref exists) the restatement is
+    byte-identical to the reference's compiled _doShuffle/_doUnshuffle and
+    _fletcher32 on random buffers of every elementsize."""
     _ref()
     import importlib
 
     mod = importlib.import_module("numcodecs._shuffle")
-    x = np.arange(4096, dtype="u1")
-    out = np.zeros_like(x)
-    mod._doShuffle(x, out, 4)
-    assert np.array_equal(out, nporacle.shuffle(x, 4))
+    rng = np.random.default_rng(5)
+    for es in (2, 3, 4, 8, 16):
+        x = rng.integers(0, 256, es * 4099, dtype=np.uint8)
+        a, b = np.zeros_like(x), np.zeros_like(x)
+        mod._doShuffle(x, a, es)
+        nporacle.shuffle_into(x, b, es)
+        assert np.array_equal(a, b)
+        mod._doUnshuffle(x, a, es)
+        nporacle.unshuffle_into(x, b, es)
+        assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------------------
+# the scalar C restatement timed as bench.py's cpu_baseline (oracle/ncoracle.c)
+# ---------------------------------------------------------------------------
+def test_c_restatement_bitround32_goldens():
+    n = 0
+    for i, m in enumerate(MANIFEST["bitround"]):
+        if m["dtype"] != "<f4":
+            continue
+        x = vec(DATA, "bitround", i, "input").view("<u4")
+        out = np.empty_like(x)
+        nporacle.c_bitround32_into(x, out, m["keepbits"])
+        assert out.tobytes() == vec(DATA, "bitround", i, "encoded").tobytes(), m
+        n += 1
+    assert n >= 6
+
+
+def test_c_restatement_fso_f4_i2_goldens():
+    n = 0
+    for i, m in enumerate(MANIFEST["fso"]):
+        if (m["dtype"], m["astype"]) != ("<f4", "<i2"):
+            continue
+        x = vec(DATA, "fso", i, "input").view("<f4")
+        enc = np.empty(x.size, dtype="<i2")
+        nporacle.c_fso_encode_f4_i2_into(x, enc, m["offset"], m["scale"])
+        assert enc.tobytes() == vec(DATA, "fso", i, "encoded").tobytes(), m
+        dec = np.empty(x.size, dtype="<f4")
+        nporacle.c_fso_decode_i2_f4_into(enc, dec, m["offset"], m["scale"])
+        exp = oracle.fso_decode(enc, m["offset"], m["scale"], "<f4", "<i2")
+        assert dec.tobytes() == exp.tobytes(), m
+        n += 1
+    assert n == 2
+
+
+def test_c_restatement_fso_decode_every_int16():
+    """(enc / scale) + offset in float64 -> float32 for all 65536 int16 values."""
+    enc = np.arange(-32768, 32768, dtype="<i2")
+    for offset, scale in ((1000, 1e3), (1000.1, 1000.0), (-3.5, 0.1), (0, 7)):
+        dec = np.empty(enc.size, dtype="<f4")
+        nporacle.c_fso_decode_i2_f4_into(enc, dec, offset, scale)
+        assert dec.tobytes() == oracle.fso_decode(enc, offset, scale, "<f4", "<i2").tobytes()
+
+
+def test_c_restatement_delta_i2_goldens_and_wrap():
+    i = next(k for k, m in enumerate(MANIFEST["delta"]) if (m["dtype"], m["astype"]) == ("<i2", "<i2"))
+    x = vec(DATA, "delta", i, "input").view("<i2")
+    enc = np.empty_like(x)
+    nporacle.c_delta_encode_i2_into(x, enc)
+    assert enc.tobytes() == vec(DATA, "delta", i, "encoded").tobytes()
+    dec = np.empty_like(x)
+    nporacle.c_delta_decode_i2_into(enc, dec)
+    assert np.array_equal(dec, x)
+    w = np.array([32767, -32768, 5, -32768, 32767, 0], dtype="<i2")
+    e2 = np.empty_like(w)
+    nporacle.c_delta_encode_i2_into(w, e2)
+    assert e2.tobytes() == oracle.delta_encode(w, "<i2").tobytes()
+
+
+def test_c_restatement_c4_chain_sha():
+    """The CPU baseline's C4 chain (FSO f4->i2, Delta i2, Shuffle 2, and back)
+    reproduces the reference's outputs on the full-size C4 input (256 MiB
+    f32, tests/golden/inputs.py), by the SHA-256 digests make_golden.py took
+    from the real reference."""
+    import hashlib
+
+    from tests.golden import inputs
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fullsize.json")) as f:
+        full = json.load(f)["C4"]
+    sha = lambda a: hashlib.sha256(a.tobytes()).hexdigest()  # noqa: E731
+    x = inputs.f32_c4(4, 64 << 20)
+    assert sha(x) == full["input"]
+    t1 = np.empty(x.size, dtype="<i2")
+    t2 = np.empty_like(t1)
+    nporacle.c_fso_encode_f4_i2_into(x, t1, 1000, 1e3)
+    assert sha(t1) == full["fso"]
+    nporacle.c_delta_encode_i2_into(t1, t2)
+    assert sha(t2) == full["delta"]
+    enc = np.empty(t2.nbytes, dtype="u1")
+    nporacle.shuffle_into(t2, enc, 2)
+    assert sha(enc) == full["shuffle2"]
+    nporacle.unshuffle_into(enc, t1, 2)
+    nporacle.c_delta_decode_i2_into(t1, t2)
+    dec = np.empty_like(x)
+    nporacle.c_fso_decode_i2_f4_into(t2, dec, 1000, 1e3)
+    assert sha(dec) == full["decoded"]
+
+
+def test_cpu_baseline_workloads_roundtrip():
+    """Every bench cpu_baseline workload decodes to the oracle's answer."""
+    from oracle import cpu_baseline
+
+    for cfg, nbytes in (("C1", 1 << 20), ("C2_f32", 1 << 20), ("C2_f64", 1 << 20), ("C3", 1 << 20),
+                        ("C4", 1 << 20), ("C5", 2 << 20)):
+        w = cpu_baseline.Workload(cfg, nbytes, seed=3)
+        w.step()
+        w.verify()

@@ -1,6 +1,6 @@
 set -u
 cd "${GRAFT_REPO_ROOT}"
-MCODEC_C4_VARIANT=1 timeout -k 10 120 python tools/probe_c4.py || exit 1
+timeout -k 10 120 python tools/probe_c4.py 67108864 1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o c4 -- python3 tools/probe_c4.py > gpurun_out/prof_c4.log 2>&1 || { echo "rocprof failed"; exit 1; }
 python3 - <<'PY'
 import csv, glob

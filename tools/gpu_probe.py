@@ -18,7 +18,10 @@ lib = ctypes.CDLL(os.path.join(ROOT, "numcodecs_amd", "_lib", "libmcodec.so"))
 V = ctypes.c_void_p
 S = ctypes.c_size_t
 I = ctypes.c_int
-lib.mc_shuffle_variant.argtypes = [V, V, S, S, I, I, I, V]
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from lab.lablib import lab as _lab  # noqa: E402  (the sweep entry points live in the lab library)
+
+lab = _lab()
 lib.mc_device_count.restype = I
 
 
@@ -48,9 +51,9 @@ def main():
             ref = x.view(count, es).t().contiguous().view(-1)
             for var in (0, 1, 2, 3, 4, 9, 10, 11):
                 y = torch.empty_like(x)
-                rc = lib.mc_shuffle_variant(x.data_ptr(), y.data_ptr(), nbytes, es, 1, var, 0, st)
+                rc = lab.mc_lab_shuffle_variant(x.data_ptr(), y.data_ptr(), nbytes, es, 1, var, 0, st)
                 z = torch.empty_like(x)
-                rc2 = lib.mc_shuffle_variant(y.data_ptr(), z.data_ptr(), nbytes, es, 0, var, 0, st)
+                rc2 = lab.mc_lab_shuffle_variant(y.data_ptr(), z.data_ptr(), nbytes, es, 0, var, 0, st)
                 torch.cuda.synchronize()
                 ok = rc == 0 and rc2 == 0 and torch.equal(y, ref) and torch.equal(z, x)
                 if not ok:
@@ -88,7 +91,7 @@ def main():
             for var in (1, 2, 3, 9, 10, 11):
                 for grid in ((0, 4096, 8192, 16384) if not quick else (0,)):
                     def fn(i, es=es, enc=enc, var=var, grid=grid):
-                        rc = lib.mc_shuffle_variant(ins[i].data_ptr(), outs[i].data_ptr(), N, es, enc, var, grid, st)
+                        rc = lab.mc_lab_shuffle_variant(ins[i].data_ptr(), outs[i].data_ptr(), N, es, enc, var, grid, st)
                         assert rc == 0, rc
                     t = timeit(fn)
                     r = {"es": es, "enc": enc, "var": var, "grid": grid, "ms": round(t * 1e3, 4),

@@ -1,0 +1,37 @@
+// lab_sweeps.hip -- LAB ONLY (libmcodec_lab.so; never part of libmcodec.so or
+// include/mcodec.h): explicit-schedule entry points used by the measurement
+// sweeps (tools/probe_enc.py, tools/gpu_probe.py, tools/probe_delta.py) and by
+// the tests that keep every schedule byte-identical to the default
+// (tests/test_gpu_sweep.py).
+#include "mc_shuffle.h"
+
+int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                               size_t nchunks, size_t n, int astype, int dtype, int variant,
+                               mc_stream_t stream);
+
+extern "C" {
+
+// Shuffle with an explicit kernel layout and grid (mc_shuffle.hip Variant):
+// bits 0-2 layout (0 default, 1 register/dword stores, 2 LDS-staged 16-B
+// stores, 3 LDS both sides, 4 generic byte kernel, 5 lane pairs), | 8
+// temporal accesses, | 16 / | 128 2x / 4x tiles, bits 5-6 tile group,
+// | 256 software-pipelined persistent loop; max_blocks 0 = default grid.
+int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize, int encode,
+                           int variant, int max_blocks, mc_stream_t stream) {
+  if (variant < 0 || (variant & 7) > 5 || (variant & ~0x1FF) != 0) return MC_EINVAL;
+  return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
+                         (hipStream_t)stream);
+}
+
+// mc_delta_decode_batch with an explicit float-chain schedule (LDS slot
+// bytes / chain values per LDS read group): 0 default (by batch size),
+// 1 32 KiB/16, 2 32 KiB/32, 3 8 KiB/16, 4 8 KiB/32, 5 4 KiB/32.  Integer
+// dtypes ignore it.  All give identical bytes.
+int mc_lab_delta_decode_batch_variant(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                                      size_t nchunks, size_t n, int astype, int dtype, int variant,
+                                      mc_stream_t stream) {
+  return mc_delta_decode_batch_impl(src, src_stride, dst, dst_stride, nchunks, n, astype, dtype, variant,
+                                    stream);
+}
+
+}  // extern "C"

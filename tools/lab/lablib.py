@@ -1,0 +1,37 @@
+"""ctypes binding of libmcodec_lab.so -- LAB ONLY (tools/, tests of the
+rejected / sweep schedules).  The lab library is the product objects plus
+tools/lab/*.hip; the product (numcodecs_amd, include/mcodec.h) never loads it.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- the HIP runtime must be torch's (see numcodecs_amd/_native.py)
+
+LAB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_build", "libmcodec_lab.so")
+
+_V, _S, _I, _D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
+_SIGS = {
+    "mc_lab_shuffle_variant": ([_V, _V, _S, _S, _I, _I, _I, _V], _I),
+    "mc_lab_delta_decode_batch_variant": ([_V, _S, _V, _S, _S, _S, _I, _I, _I, _V], _I),
+    "mc_lab_c4_decode_workspace": ([_S], _S),
+    "mc_lab_c4_decode_variant": ([_V, _V, _S, _I, _I, _D, _D, _V, _S, _I, _V], _I),
+}
+_lib = None
+
+
+def lab():
+    """The loaded lab library (built by `make -C tools/lab`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LAB_PATH):
+            raise FileNotFoundError(f"{LAB_PATH} missing: build it with `make -C tools/lab`")
+        lib = ctypes.CDLL(LAB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+    return _lib

@@ -1,6 +1,6 @@
 """C4 decode/encode with 4 rotating buffer sets (so no call finds its input in
 the 256 MiB Infinity Cache from a previous call); knobs are read once per
-process (MCODEC_C4_LOADS, MCODEC_C4_VARIANT).  One JSON line."""
+process (MCODEC_C4_LOADS).  One JSON line."""
 import json
 import os
 import sys
@@ -37,6 +37,6 @@ def timed(fn, reps=40):
 
 t_dec = timed(lambda i: pipe.decode(es[i]))
 t_enc = timed(lambda i: pipe.encode(xs[i]))
-print(json.dumps({"loads": os.environ.get("MCODEC_C4_LOADS", "0"), "variant": os.environ.get("MCODEC_C4_VARIANT", "0"),
+print(json.dumps({"loads": os.environ.get("MCODEC_C4_LOADS", "0"),
                   "ok": ok, "dec_us": round(t_dec * 1e3, 1), "enc_us": round(t_enc * 1e3, 1),
                   "encdec_GiBps": round(2 * 4 * n / (1 << 30) / ((t_dec + t_enc) / 1e3), 1)}), flush=True)

@@ -60,8 +60,11 @@ for dt, tdt in (("|i1", torch.int8), ("<i2", torch.int16), ("<i4", torch.int32),
 
     td = timed(dec, reps=6)
     out[f"single256MiB_{dt[1:]}_decode_GBps"] = round(2 * 256 * MiB / td / 1e9, 1)
-# float-chain schedules (mc_delta_decode_batch_variant)
-from numcodecs_amd._native import lib, check  # noqa: E402
+# float-chain schedules (lab: mc_lab_delta_decode_batch_variant)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+from lab.lablib import lab as _lab  # noqa: E402
+from numcodecs_amd._native import check  # noqa: E402
+lib = _lab()
 from numcodecs_amd._ops import dtype_code  # noqa: E402
 import numpy as np  # noqa: E402
 
@@ -75,7 +78,7 @@ for dt, tdt in (("<f4", torch.float32), ("<f8", torch.float64)):
         y = torch.empty_like(x)
         ref = None
         for v in range(6):
-            f = lambda: check(lib.mc_delta_decode_batch_variant(x.data_ptr(), n * es, y.data_ptr(), n * es, rows, n,
+            f = lambda: check(lib.mc_lab_delta_decode_batch_variant(x.data_ptr(), n * es, y.data_ptr(), n * es, rows, n,
                                                                   code, code, v, st), "variant")
             t = timed(f, reps=2)
             if ref is None:

@@ -13,7 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 lib = ctypes.CDLL(os.path.join(ROOT, "numcodecs_amd", "_lib", "libmcodec.so"))
 bw = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libbwtest.so"))
 V, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-lib.mc_shuffle_variant.argtypes = [V, V, S, S, I, I, I, V]
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from lab.lablib import lab as _lab  # noqa: E402  (the sweep entry points live in the lab library)
+
+lab = _lab()
 bw.bw_copy.argtypes = [V, V, S, I, I, V]
 
 
@@ -43,7 +46,7 @@ def main():
         if kind == "copy-nt":
             assert bw.bw_copy(ins[i].data_ptr(), outs[i].data_ptr(), n, 2, grid, st) == 0
         else:
-            assert lib.mc_shuffle_variant(ins[i].data_ptr(), outs[i].data_ptr(), n, es, enc, var, grid, st) == 0
+            assert lab.mc_lab_shuffle_variant(ins[i].data_ptr(), outs[i].data_ptr(), n, es, enc, var, grid, st) == 0
 
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -67,7 +70,7 @@ def main():
             continue
         y = torch.empty(n, dtype=torch.uint8, device=dev)
         src = x[:n] if enc else x[:n].view(n // es, es).t().contiguous().view(-1)
-        assert lib.mc_shuffle_variant(src.data_ptr(), y.data_ptr(), n, es, enc, var, grid, st) == 0
+        assert lab.mc_lab_shuffle_variant(src.data_ptr(), y.data_ptr(), n, es, enc, var, grid, st) == 0
         ref = x[:n].view(n // es, es).t().contiguous().view(-1) if enc else x[:n]
         if not torch.equal(y, ref):
             bad.append(c)
