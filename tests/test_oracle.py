@@ -227,8 +227,10 @@ def test_golden_inputs_portable():
 # direct comparison with the real reference (this container only)
 # ---------------------------------------------------------------------------
 def _ref():
-    from oracle import refload
-
+    try:
+        from oracle import refload
+    except ImportError:  # the reference loader stays in the build container (.gpurunignore)
+        pytest.skip("reference loader not present (GPU box)")
     if not refload.available():
         pytest.skip("reference sources / oracle/_ref build not present (GPU box)")
     return refload.load()

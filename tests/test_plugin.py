@@ -76,8 +76,10 @@ def test_entry_point_plugin(tmp_path, monkeypatch):
 
 
 def test_register_with_reference_numcodecs():
-    from oracle import refload
-
+    try:
+        from oracle import refload
+    except ImportError:  # the reference loader stays in the build container (.gpurunignore)
+        pytest.skip("reference loader not present (GPU box)")
     if not refload.available():
         pytest.skip("reference sources not present (GPU box)")
     ref = refload.load()

@@ -2,7 +2,7 @@
 # Run a sequence of GPU steps on the box, each under its own time limit; stop
 # at the first step that crashes, aborts or times out (exit 124/134/137/139),
 # continue past ordinary test failures.  Usage: tools/gpu_session.sh STEP...
-# where STEP is one of: tests, smoke, bench, benchx, probe, rocprof, pmc
+# where STEP is one of: tests, smoke, bench, benchq, benchprof, pmcall, multi, probe, rocprof, pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -20,22 +20,20 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    benchprof) run rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o bench -- python3 bench.py ;;
-    benchx) run bench_extra 900 python bench.py --extra --no-cpu ;;
-    profx) run rocprof_extra 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_extra -o bench -- python3 bench.py --extra --no-cpu --steps 10 ;;
-    pmcx) run pmc_fetch_x 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
-               -d gpurun_out/prof_fetch_extra -o bench -- python3 bench.py --extra --no-cpu --steps 5 --warmup 1
-          run pmc_write_x 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
-               -d gpurun_out/prof_write_extra -o bench -- python3 bench.py --extra --no-cpu --steps 5 --warmup 1 ;;
-    e2e) run bench_e2e 900 python bench.py --e2e --no-cpu --steps 20 ;;
-    multi) run bench_multi2 600 env MCODEC_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 50 --warmup 5 ;;
+    benchq) run bench_quick 600 python bench.py --no-cpu --quick ;;
+    benchprof) run rocprof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt_all -o bench -- python3 bench.py --no-cpu --steps 20 --warmup 5 ;;
+    pmcall) run pmc_fetch_all 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_fetch_all -o bench -- python3 bench.py --no-cpu --steps 5 --warmup 1
+          run pmc_write_all 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+               -d gpurun_out/prof_write_all -o bench -- python3 bench.py --no-cpu --steps 5 --warmup 1 ;;
+    multi) run bench_multi2 600 env MCODEC_BENCH_BACKEND=gloo python bench.py --gpus 2 --no-cpu --quick --steps 50 --warmup 5 ;;
     probe) run probe_enc4 600 python tools/probe_enc.py 4 ;;
     rocprof) run rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
-               -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --steps 50 --warmup 5 ;;
+               -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --quick --steps 50 --warmup 5 ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
-               -d gpurun_out/prof_fetch -o bench -- python3 bench.py --no-cpu --steps 20 --warmup 2
+               -d gpurun_out/prof_fetch -o bench -- python3 bench.py --no-cpu --quick --steps 20 --warmup 2
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
-               -d gpurun_out/prof_write -o bench -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
+               -d gpurun_out/prof_write -o bench -- python3 bench.py --no-cpu --quick --steps 20 --warmup 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
