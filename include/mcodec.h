@@ -137,6 +137,22 @@ size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
                     int dtype, void *workspace, size_t workspace_bytes,
                     mc_stream_t stream);
+/* Same-width integer decodes (astype == dtype of 1, 2 or 4 bytes, n *
+ * itemsize % 16 == 0, 16-B aligned buffers) run as ONE pass over the encoded
+ * bytes: partitions held in LDS across a decoupled look-back, 2N of HBM
+ * traffic instead of the 3N of a reduce-then-scan.  The look-back needs
+ * `state`: mc_delta_decode_state_bytes() device bytes (0 = this shape has no
+ * single-pass decode), 16-B aligned, that are ZERO before the first call and
+ * that every completed call leaves zero again -- keep one per stream.
+ * mc_delta_decode zeroes the leading state bytes of its workspace itself
+ * (one hipMemsetAsync per call); mc_delta_decode_state skips that.  Shapes
+ * that do not take the single pass fall back to mc_delta_decode with
+ * `workspace`. */
+size_t mc_delta_decode_state_bytes(size_t n, int astype, int dtype);
+int mc_delta_decode_state(const void *src, void *dst, size_t n, int astype,
+                          int dtype, void *state, size_t state_bytes,
+                          void *workspace, size_t workspace_bytes,
+                          mc_stream_t stream);
 /* Batched Delta over nchunks chunks of n elements each (chunk c read at
  * src + c*src_stride, written at dst + c*dst_stride; strides in bytes).
  * Each chunk is an independent Delta (its own first element / cumsum).
@@ -263,6 +279,17 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
                                 int astype, int dtype, double scale,
                                 double offset, void *workspace,
                                 size_t workspace_bytes, mc_stream_t stream);
+/* The same decode with a persistent single-pass state (the contract of
+ * mc_delta_decode_state: zero before the first call, left zero by every
+ * call, one per stream); falls back to mc_fso_delta_shuffle_decode with
+ * `workspace` when no state is given. */
+size_t mc_fso_delta_shuffle_decode_state_bytes(size_t n, int astype);
+int mc_fso_delta_shuffle_decode_state(const void *src, void *dst, size_t n,
+                                      int astype, int dtype, double scale,
+                                      double offset, void *state,
+                                      size_t state_bytes, void *workspace,
+                                      size_t workspace_bytes,
+                                      mc_stream_t stream);
 
 /* ---- Checksum32 family (checksum32.py:45-209, jenkins.pyx:93-325) ------- */
 /* One 32-bit checksum per chunk of a batch (rows at src + c*src_stride):

@@ -81,6 +81,8 @@ _SIGNATURES = {
     "mc_delta_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_workspace": [_c_size, _c_int, _c_int],
     "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
+    "mc_delta_decode_state_bytes": [_c_size, _c_int, _c_int],
+    "mc_delta_decode_state": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
     "mc_delta_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch_workspace": [_c_size, _c_size, _c_int, _c_int],
@@ -112,6 +114,10 @@ _SIGNATURES = {
     ],
     "mc_fso_delta_shuffle_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp],
     "mc_fso_delta_shuffle_decode_workspace": [_c_size],
+    "mc_fso_delta_shuffle_decode_state_bytes": [_c_size, _c_int],
+    "mc_fso_delta_shuffle_decode_state": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp, _c_size, _c_vp,
+    ],
     "mc_fso_delta_shuffle_decode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
     ],
@@ -141,6 +147,8 @@ _RESTYPES = {
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
     "mc_fso_delta_shuffle_decode_workspace": ctypes.c_size_t,
+    "mc_fso_delta_shuffle_decode_state_bytes": ctypes.c_size_t,
+    "mc_delta_decode_state_bytes": ctypes.c_size_t,
     "mc_checksum32_workspace": ctypes.c_size_t,
 }
 

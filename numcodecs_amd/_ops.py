@@ -46,6 +46,31 @@ def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
 
 
+# Persistent single-pass scan states (include/mcodec.h, mc_delta_decode_state):
+# device bytes that are zero before the first call and that every call leaves
+# zero, so they are kept per (device, stream) and never re-zeroed.  A state
+# is never created during HIP-graph capture (nothing runs at capture time, so
+# its zero fill would not have happened); captured decodes take the plain
+# entry points, which zero their workspace in the graph.
+_STATES: "dict[tuple[int, int], torch.Tensor]" = {}
+
+
+def scan_state(nbytes: int, like: torch.Tensor):
+    """A zeroed single-pass scan state of at least `nbytes` for torch's
+    current stream on `like`'s device, or None (nbytes == 0, or capturing)."""
+    if nbytes == 0 or torch.cuda.is_current_stream_capturing():
+        return None
+    key = (like.device.index, stream(like))
+    st = _STATES.get(key)
+    if st is None or st.numel() < nbytes:
+        # grown geometrically; the old state is released (calls on this
+        # stream are ordered, so nothing still uses it)
+        size = max(int(nbytes), 2 * st.numel() if st is not None else 1 << 16)
+        st = torch.zeros(size, dtype=torch.uint8, device=like.device)
+        _STATES[key] = st
+    return st
+
+
 _NO_GUARD = contextlib.nullcontext()
 
 
@@ -140,6 +165,12 @@ def delta_decode(src, dst, n, astype, dtype) -> None:
         return
     with _guard(src):
         a, d = dtype_code(astype), dtype_code(dtype)
+        st = scan_state(lib.mc_delta_decode_state_bytes(n, a, d), src)
+        if st is not None and src.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0:
+            # single pass with the stream's persistent state: no workspace
+            check(lib.mc_delta_decode_state(src.data_ptr(), dst.data_ptr(), n, a, d, st.data_ptr(), st.numel(),
+                                            None, 0, stream(src)), "mc_delta_decode_state")
+            return
         ws_n = lib.mc_delta_decode_workspace(n, a, d)
         ws = workspace(ws_n, src)
         check(lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d, ws.data_ptr(), ws.numel(),

@@ -77,13 +77,12 @@ MC_DEV void unpack_quad(const uint32_t (&w)[ES], int64_t (&d)[4]) {
 // (lane-contiguous) load per plane, 4 quads unshuffled in registers.
 constexpr int C4_PER = 16;
 
+// the 16 deltas of one unit from its ES plane vectors (dword c of every
+// plane = elements 4c..4c+3), as astype values widened to 32 bits
 template <int A, int ES>
-MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)[C4_PER]) {
-  mc_u32x4 pl[ES];
+MC_DEV void c4_planes_to_deltas(const mc_u32x4 (&pl)[ES], uint32_t (&v)[C4_PER]) {
 #pragma unroll
-  for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<true>(src + (size_t)b * n + e0);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {  // dword c of every plane = elements 4c..4c+3
+  for (int c = 0; c < 4; ++c) {
     uint32_t pq[ES], w[ES];
 #pragma unroll
     for (int b = 0; b < ES; ++b) pq[b] = pl[b][c];
@@ -93,6 +92,14 @@ MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[4 * c + k] = (uint32_t)d[k];
   }
+}
+
+template <int A, int ES>
+MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)[C4_PER]) {
+  mc_u32x4 pl[ES];
+#pragma unroll
+  for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<true>(src + (size_t)b * n + e0);
+  c4_planes_to_deltas<A, ES>(pl, v);
 }
 
 // scan of 16 consecutive deltas + FSO decode, staged through LDS for
@@ -153,6 +160,9 @@ MC_DEV void c4_local_scan(const uint8_t *src, size_t tile, const C4Params &p, ui
     v[k] = run;
   }
 }
+
+template <int A>
+constexpr int c4_es() { return A == MC_I2 || A == MC_U2 ? 2 : 4; }
 
 static inline bool c4_ok(const void *src, const void *dst, size_t n, int dtype, int astype) {
   if (!(dtype == MC_F4 || dtype == MC_F8)) return false;

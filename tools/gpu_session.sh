@@ -28,6 +28,10 @@ for step in "$@"; do
                -d gpurun_out/prof_write_all -o bench -- python3 bench.py --no-cpu --steps 5 --warmup 1 ;;
     multi) run bench_multi2 600 env MCODEC_BENCH_BACKEND=gloo python bench.py --gpus 2 --no-cpu --quick --steps 50 --warmup 5 ;;
     probe) run probe_enc4 600 python tools/probe_enc.py 4 ;;
+    t1p) run pytest_scan1p 600 python -u -m pytest tests/test_gpu_scan1p.py tests/test_gpu_c4.py tests/test_gpu_delta.py tests/test_gpu_fullsize.py -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf ;;
+    p1p) run probe_scan1p 300 python tools/probe_scan1p.py
+         run probe_scan3p 300 env MCODEC_SCAN1P=0 python tools/probe_scan1p.py ;;
+    prof1p) run rocprof_scan1p 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_scan1p -o scan -- python3 tools/probe_scan1p.py ;;
     rocprof) run rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
                -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --quick --steps 50 --warmup 5 ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \

@@ -3,7 +3,7 @@
 // schedules that DESIGN.md measured against the product's 3-pass scans.
 #pragma once
 
-#include "mc_scan.h"
+#include "mc_lookback.h"
 
 // ---------------------------------------------------------------------------
 // Decoupled look-back (single-pass scan across workgroups).
@@ -21,11 +21,6 @@
 // that into an error).  The counter and the status words are zeroed by a
 // hipMemsetAsync on the stream before every launch.
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) uint64_t mc_gu64;
-typedef __attribute__((address_space(1))) uint32_t mc_gu32;
-
-constexpr uint64_t MC_LB_AGG = 1ull << 32;
-constexpr uint64_t MC_LB_INC = 2ull << 32;
 constexpr unsigned MC_LB_SPIN_LIMIT = 1u << 22;
 
 // thread 0 of a block: the block's tile index (broadcast through `slot`)
@@ -79,7 +74,6 @@ MC_DEV uint32_t mc_lb_lookback(uint64_t *status_, size_t tile, uint32_t aggregat
 // false (wave-uniform) and nothing more is published: the caller then derives
 // the prefix from the data itself and publishes it (always correct, whatever
 // the dispatch order).
-constexpr unsigned MC_LB_WAVE_SPINS = 1u << 14;
 
 template <bool OR_OP>
 MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t aggregate, bool &ok,
@@ -127,79 +121,6 @@ MC_DEV uint32_t mc_lb_lookback_wave(uint64_t *status_, size_t tile, uint32_t agg
     __hip_atomic_store(&status[tile], MC_LB_INC | incv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return prefix;
-}
-
-// Wider variant for coarse partitions: every lane reads 4 consecutive
-// predecessors per round (256 per round, the 4 loads in flight together), so
-// the walk back to the nearest inclusive prefix takes distance/256 round
-// trips.  Same contract as mc_lb_lookback_wave.
-template <bool OR_OP>
-MC_DEV uint32_t mc_lb_lookback_wave4(uint64_t *status_, size_t tile, uint32_t aggregate, bool &ok,
-                                     unsigned max_spins = MC_LB_WAVE_SPINS) {
-  mc_gu64 *status = (mc_gu64 *)status_;
-  const int lane = threadIdx.x & 63;
-  ok = true;
-  if (tile == 0) {
-    if (lane == 0)
-      __hip_atomic_store(&status[0], MC_LB_INC | aggregate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  if (lane == 0)
-    __hip_atomic_store(&status[tile], MC_LB_AGG | aggregate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t prefix = 0;
-  long long base = (long long)tile - 1;  // nearest predecessor: lane 0, slot 0
-  unsigned spins = 0;
-  for (;;) {
-    uint64_t s[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long long idx = base - 4 * lane - q;
-      s[q] = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : MC_LB_INC;  // before tile 0: an inclusive prefix of 0
-    }
-    bool pending = false;
-    int fq = 4;  // this lane's nearest inclusive slot
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t flag = (uint32_t)(s[q] >> 32);
-      pending |= flag == 0;
-      if (fq == 4 && flag == 2) fq = q;
-    }
-    if (__any(pending)) {
-      if (++spins > max_spins) {
-        ok = false;
-        return 0;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    const unsigned long long inc = __ballot(fq < 4);
-    const int first = inc ? __ffsll((long long)inc) - 1 : 64;  // nearest lane holding an inclusive
-    uint32_t v = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool take = lane < first || (lane == first && q <= fq);
-      if (take) v = OR_OP ? (v | (uint32_t)s[q]) : (v + (uint32_t)s[q]);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t o = __shfl_xor(v, off, 64);
-      v = OR_OP ? (v | o) : (v + o);
-    }
-    prefix = OR_OP ? (prefix | v) : (prefix + v);
-    if (inc) break;
-    base -= 256;
-  }
-  if (lane == 0) {
-    const uint32_t incv = OR_OP ? (prefix | aggregate) : (prefix + aggregate);
-    __hip_atomic_store(&status[tile], MC_LB_INC | incv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return prefix;
-}
-
-MC_DEV void mc_lb_publish_inclusive(uint64_t *status_, size_t tile, uint32_t inclusive) {
-  __hip_atomic_store(&((mc_gu64 *)status_)[tile], MC_LB_INC | inclusive, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // workspace layout for a look-back scan over ntiles tiles:

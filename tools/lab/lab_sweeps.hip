@@ -9,7 +9,25 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
                                size_t nchunks, size_t n, int astype, int dtype, int variant,
                                mc_stream_t stream);
 
+int mc_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, hipStream_t st, unsigned spins);
+int mc_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype, double scale, double offset,
+                void *state, hipStream_t st, unsigned spins);
+
 extern "C" {
+
+// The product's single-pass decodes (mc_scan1p.hip) with an explicit
+// look-back spin bound: 0 makes every partition whose predecessors have not
+// all published yet take the data-derived prefix (the guard path), so tests
+// can check that path byte for byte.  `state` as for mc_delta_decode_state.
+int mc_lab_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, unsigned spins,
+                       mc_stream_t stream) {
+  return mc_delta_dec1p(src, dst, n, es, state, (hipStream_t)stream, spins);
+}
+
+int mc_lab_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype, double scale, double offset,
+                    void *state, unsigned spins, mc_stream_t stream) {
+  return mc_c4_dec1p(src, dst, n, astype, dtype, scale, offset, state, (hipStream_t)stream, spins);
+}
 
 // Shuffle with an explicit kernel layout and grid (mc_shuffle.hip Variant):
 // bits 0-2 layout (0 default, 1 register/dword stores, 2 LDS-staged 16-B
