@@ -137,22 +137,6 @@ size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
                     int dtype, void *workspace, size_t workspace_bytes,
                     mc_stream_t stream);
-/* Same-width integer decodes (astype == dtype of 1, 2 or 4 bytes, n *
- * itemsize % 16 == 0, 16-B aligned buffers) run as ONE pass over the encoded
- * bytes: partitions held in LDS across a decoupled look-back, 2N of HBM
- * traffic instead of the 3N of a reduce-then-scan.  The look-back needs
- * `state`: mc_delta_decode_state_bytes() device bytes (0 = this shape has no
- * single-pass decode), 16-B aligned, that are ZERO before the first call and
- * that every completed call leaves zero again -- keep one per stream.
- * mc_delta_decode zeroes the leading state bytes of its workspace itself
- * (one hipMemsetAsync per call); mc_delta_decode_state skips that.  Shapes
- * that do not take the single pass fall back to mc_delta_decode with
- * `workspace`. */
-size_t mc_delta_decode_state_bytes(size_t n, int astype, int dtype);
-int mc_delta_decode_state(const void *src, void *dst, size_t n, int astype,
-                          int dtype, void *state, size_t state_bytes,
-                          void *workspace, size_t workspace_bytes,
-                          mc_stream_t stream);
 /* Batched Delta over nchunks chunks of n elements each (chunk c read at
  * src + c*src_stride, written at dst + c*dst_stride; strides in bytes).
  * Each chunk is an independent Delta (its own first element / cumsum).
@@ -214,6 +198,16 @@ int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes,
 int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair,
                          void *workspace, size_t workspace_bytes,
                          mc_stream_t stream);
+/* mc_fletcher32_verify in ONE launch: the checksum's last block folds the
+ * partials (no finalize kernel).  `ticket`: 16 device uint32 words (an
+ * arrival counter), zero before the first call and left zero by every call
+ * (keep one per stream);
+ * NULL = mc_fletcher32_verify.  out_pair may be host-mapped pinned memory
+ * (hipHostMalloc): the caller then reads the verdict after one stream sync,
+ * with no device-to-host copy. */
+int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_pair,
+                               void *workspace, size_t workspace_bytes,
+                               uint32_t *ticket, mc_stream_t stream);
 /* out_sums[c] = fletcher32(chunk c), chunk c = src + c*stride, chunk_bytes. */
 size_t mc_fletcher32_batch_workspace(size_t nchunks, size_t chunk_bytes);
 int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks,
@@ -279,17 +273,6 @@ int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
                                 int astype, int dtype, double scale,
                                 double offset, void *workspace,
                                 size_t workspace_bytes, mc_stream_t stream);
-/* The same decode with a persistent single-pass state (the contract of
- * mc_delta_decode_state: zero before the first call, left zero by every
- * call, one per stream); falls back to mc_fso_delta_shuffle_decode with
- * `workspace` when no state is given. */
-size_t mc_fso_delta_shuffle_decode_state_bytes(size_t n, int astype);
-int mc_fso_delta_shuffle_decode_state(const void *src, void *dst, size_t n,
-                                      int astype, int dtype, double scale,
-                                      double offset, void *state,
-                                      size_t state_bytes, void *workspace,
-                                      size_t workspace_bytes,
-                                      mc_stream_t stream);
 
 /* ---- Checksum32 family (checksum32.py:45-209, jenkins.pyx:93-325) ------- */
 /* One 32-bit checksum per chunk of a batch (rows at src + c*src_stride):
@@ -342,6 +325,26 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride,
                                int location, uint32_t *out_sums,
                                uint32_t *out_stored, void *workspace,
                                size_t workspace_bytes, mc_stream_t stream);
+
+/* Checksum32.decode's verification of ONE encoded buffer (payload + 4 bytes
+ * at `location`) in one launch: out_pair[0] = checksum of the payload,
+ * out_pair[1] = the stored LE32 value (the caller compares and raises).
+ * `ticket` and out_pair as for mc_fletcher32_verify_fused; workspace:
+ * mc_checksum32_workspace(kind, 1, encoded_bytes - 4). */
+int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes,
+                               uint32_t init, const void *prefix,
+                               size_t prefix_bytes, int location,
+                               uint32_t *out_pair, void *workspace,
+                               size_t workspace_bytes, uint32_t *ticket,
+                               mc_stream_t stream);
+
+/* hipStreamSynchronize(stream) (the codecs' one host wait per verified
+ * decode); returns a status. */
+int mc_stream_synchronize(mc_stream_t stream);
+/* The device address of mapped pinned host memory (hipHostGetDevicePointer),
+ * NULL if `host` is not mapped: where a kernel may write a host-visible
+ * verdict. */
+void *mc_host_device_pointer(void *host);
 
 /* ---- PackBits (packbits.py:33-82) --------------------------------------- */
 /* encode n bools (any nonzero byte is True) into dst[0] = padding bits

@@ -81,8 +81,6 @@ _SIGNATURES = {
     "mc_delta_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_workspace": [_c_size, _c_int, _c_int],
     "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
-    "mc_delta_decode_state_bytes": [_c_size, _c_int, _c_int],
-    "mc_delta_decode_state": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
     "mc_delta_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch_workspace": [_c_size, _c_size, _c_int, _c_int],
@@ -101,6 +99,7 @@ _SIGNATURES = {
     "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_verify": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_verify_fused": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp, _c_vp],
     "mc_fletcher32_batch_workspace": [_c_size, _c_size],
     "mc_fletcher32_batch": [_c_vp, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp, _c_size, _c_vp],
@@ -114,10 +113,6 @@ _SIGNATURES = {
     ],
     "mc_fso_delta_shuffle_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp],
     "mc_fso_delta_shuffle_decode_workspace": [_c_size],
-    "mc_fso_delta_shuffle_decode_state_bytes": [_c_size, _c_int],
-    "mc_fso_delta_shuffle_decode_state": [
-        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp, _c_size, _c_vp,
-    ],
     "mc_fso_delta_shuffle_decode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
     ],
@@ -133,6 +128,11 @@ _SIGNATURES = {
         _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_int,
         _c_vp, _c_vp, _c_vp, _c_size, _c_vp,
     ],
+    "mc_checksum32_verify_fused": [
+        _c_int, _c_vp, _c_size, _c_u32, _c_vp, _c_size, _c_int, _c_vp, _c_vp, _c_size, _c_vp, _c_vp,
+    ],
+    "mc_stream_synchronize": [_c_vp],
+    "mc_host_device_pointer": [_c_vp],
     "mc_packbits": [_c_vp, _c_vp, _c_size, _c_vp],
     "mc_copy": [_c_vp, _c_vp, _c_size, _c_vp],
     "mc_copy_rows": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp],
@@ -140,6 +140,7 @@ _SIGNATURES = {
     "mc_unpackbits": [_c_vp, _c_size, _c_vp, _c_size, _c_vp],
 }
 _RESTYPES = {
+    "mc_host_device_pointer": ctypes.c_void_p,
     "mc_strerror": ctypes.c_char_p,
     "mc_delta_decode_workspace": ctypes.c_size_t,
     "mc_delta_decode_batch_workspace": ctypes.c_size_t,
@@ -147,8 +148,6 @@ _RESTYPES = {
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
     "mc_fso_delta_shuffle_decode_workspace": ctypes.c_size_t,
-    "mc_fso_delta_shuffle_decode_state_bytes": ctypes.c_size_t,
-    "mc_delta_decode_state_bytes": ctypes.c_size_t,
     "mc_checksum32_workspace": ctypes.c_size_t,
 }
 

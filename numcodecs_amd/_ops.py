@@ -46,29 +46,48 @@ def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
 
 
-# Persistent single-pass scan states (include/mcodec.h, mc_delta_decode_state):
-# device bytes that are zero before the first call and that every call leaves
-# zero, so they are kept per (device, stream) and never re-zeroed.  A state
-# is never created during HIP-graph capture (nothing runs at capture time, so
-# its zero fill would not have happened); captured decodes take the plain
-# entry points, which zero their workspace in the graph.
-_STATES: "dict[tuple[int, int], torch.Tensor]" = {}
+class _VerifySlot:
+    """Per-(device, stream) resources of the one-launch checksum verify: a
+    zeroed arrival counter (left zero by every call), a reusable partials
+    workspace and a pinned host pair the kernel writes its verdict into."""
+
+    def __init__(self, device):
+        self.device = device
+        self.ticket = torch.zeros(16, dtype=torch.int32, device=device)  # MC_ARRIVAL_WORDS
+        self.ws = torch.empty(1 << 20, dtype=torch.uint8, device=device)
+        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self.host_np = self.host.numpy().view(np.uint32)
+        # the kernel writes the verdict through the pinned buffer's device
+        # address; if it is not mapped, into device memory + one async copy
+        self.out_ptr = lib.mc_host_device_pointer(self.host.data_ptr())
+        self.dev = None if self.out_ptr else torch.zeros(2, dtype=torch.int32, device=device)
+        if self.dev is not None:
+            self.out_ptr = self.dev.data_ptr()
+
+    def read(self, st):
+        if self.dev is not None:
+            self.host.copy_(self.dev, non_blocking=True)
+        check(lib.mc_stream_synchronize(st), "mc_stream_synchronize")
+        return int(self.host_np[0]), int(self.host_np[1])
+
+    def workspace(self, nbytes):
+        if self.ws.numel() < nbytes:
+            self.ws = torch.empty(max(int(nbytes), 2 * self.ws.numel()), dtype=torch.uint8, device=self.device)
+        return self.ws
 
 
-def scan_state(nbytes: int, like: torch.Tensor):
-    """A zeroed single-pass scan state of at least `nbytes` for torch's
-    current stream on `like`'s device, or None (nbytes == 0, or capturing)."""
-    if nbytes == 0 or torch.cuda.is_current_stream_capturing():
+_VERIFY: "dict[tuple[int, int], _VerifySlot]" = {}
+
+
+def _verify_slot(t: torch.Tensor, st: int):
+    """The stream's verify slot, or None during HIP-graph capture."""
+    if torch.cuda.is_current_stream_capturing():
         return None
-    key = (like.device.index, stream(like))
-    st = _STATES.get(key)
-    if st is None or st.numel() < nbytes:
-        # grown geometrically; the old state is released (calls on this
-        # stream are ordered, so nothing still uses it)
-        size = max(int(nbytes), 2 * st.numel() if st is not None else 1 << 16)
-        st = torch.zeros(size, dtype=torch.uint8, device=like.device)
-        _STATES[key] = st
-    return st
+    key = (t.device.index, st)
+    sl = _VERIFY.get(key)
+    if sl is None:
+        sl = _VERIFY[key] = _VerifySlot(t.device)
+    return sl
 
 
 _NO_GUARD = contextlib.nullcontext()
@@ -165,12 +184,6 @@ def delta_decode(src, dst, n, astype, dtype) -> None:
         return
     with _guard(src):
         a, d = dtype_code(astype), dtype_code(dtype)
-        st = scan_state(lib.mc_delta_decode_state_bytes(n, a, d), src)
-        if st is not None and src.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0:
-            # single pass with the stream's persistent state: no workspace
-            check(lib.mc_delta_decode_state(src.data_ptr(), dst.data_ptr(), n, a, d, st.data_ptr(), st.numel(),
-                                            None, 0, stream(src)), "mc_delta_decode_state")
-            return
         ws_n = lib.mc_delta_decode_workspace(n, a, d)
         ws = workspace(ws_n, src)
         check(lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d, ws.data_ptr(), ws.numel(),
@@ -239,9 +252,17 @@ def fletcher32_encode(src, dst, nbytes) -> None:
 
 
 def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
-    """(computed, stored) for a buffer of payload + 4-byte footer (syncs)."""
+    """(computed, stored) for a buffer of payload + 4-byte footer (syncs):
+    one launch writing its verdict into pinned host memory, one stream sync."""
     _native.require_device()
     with _guard(src):
+        st = stream(src)
+        sl = _verify_slot(src, st)
+        if sl is not None:
+            ws = sl.workspace(lib.mc_fletcher32_workspace(nbytes))
+            check(lib.mc_fletcher32_verify_fused(src.data_ptr(), nbytes, sl.out_ptr, ws.data_ptr(),
+                                                 ws.numel(), sl.ticket.data_ptr(), st), "mc_fletcher32_verify_fused")
+            return sl.read(st)
         ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
         pair = torch.empty(2, dtype=torch.int32, device=src.device)
         check(lib.mc_fletcher32_verify(src.data_ptr(), nbytes, pair.data_ptr(), ws.data_ptr(),
@@ -335,9 +356,19 @@ def checksum32_verify(kind, src, encoded_bytes, init, location, prefix=None) -> 
     """(computed, stored) checksum of ONE encoded buffer (payload + 4 bytes
     at `location`), from one mc_checksum32_decode_batch call (syncs)."""
     _native.require_device()
-    pair = torch.empty(2, dtype=torch.int32, device=src.device)
     with _guard(src):
         pre = _prefix_dev(prefix, src)
+        st = stream(src)
+        sl = _verify_slot(src, st)
+        if sl is not None:  # one launch, verdict into pinned host memory, one sync
+            ws = sl.workspace(lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4))
+            check(lib.mc_checksum32_verify_fused(kind, src.data_ptr(), encoded_bytes, init & 0xFFFFFFFF,
+                                                 pre.data_ptr() if pre is not None else None,
+                                                 pre.numel() if pre is not None else 0, location,
+                                                 sl.out_ptr, ws.data_ptr(), ws.numel(),
+                                                 sl.ticket.data_ptr(), st), "mc_checksum32_verify_fused")
+            return sl.read(st)
+        pair = torch.empty(2, dtype=torch.int32, device=src.device)
         ws = workspace(lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4), src)
         check(lib.mc_checksum32_decode_batch(kind, src.data_ptr(), encoded_bytes, None, 0, 1, encoded_bytes,
                                              init & 0xFFFFFFFF, pre.data_ptr() if pre is not None else None,

@@ -437,13 +437,6 @@ def _fso_delta_shuffle_decode(fso, delta, sh, x):
     out = torch.empty(n * fso.dtype.itemsize, dtype=torch.uint8, device=raw.device)
     _native.require_device()
     with torch.cuda.device(raw.device):
-        at, dt = _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype)
-        st = _ops.scan_state(lib.mc_fso_delta_shuffle_decode_state_bytes(n, at), raw)
-        if st is not None:  # single pass with the stream's persistent state
-            check(lib.mc_fso_delta_shuffle_decode_state(raw.data_ptr(), out.data_ptr(), n, at, dt, sc3, off4,
-                                                        st.data_ptr(), st.numel(), None, 0, _ops.stream(raw)),
-                  "mc_fso_delta_shuffle_decode_state")
-            return out.view(torch_dtype(fso.dtype))
         ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_workspace(n), raw)
         check(lib.mc_fso_delta_shuffle_decode(raw.data_ptr(), out.data_ptr(), n,
                                               _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype),

@@ -19,7 +19,6 @@
 //   measured slower and live in tools/lab/lab_c4.hip, outside this library.)
 // Bit-exact with the reference sequence of codecs (tests/test_gpu_c4.py).
 #include "mc_c4.h"
-#include "mc_lookback.h"
 
 namespace {
 
@@ -148,14 +147,6 @@ static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Para
 
 }  // namespace
 
-// single-pass decode (mc_scan1p.hip)
-bool mc_scan1p_enabled();
-size_t mc_c4_dec1p_state_bytes(size_t n, int astype);
-int mc_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype, double scale, double offset,
-                void *state, hipStream_t st, unsigned spins = MC_LB_WAVE_SPINS);
-int mc_c4_decode_three_pass(const void *src, void *dst, size_t n, int astype, int dtype, double scale,
-                            double offset, void *workspace, size_t workspace_bytes, mc_stream_t stream);
-
 extern "C" {
 
 int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype, int astype,
@@ -175,55 +166,14 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
   return mc_last_launch();
 }
 
-size_t mc_fso_delta_shuffle_decode_state_bytes(size_t n, int astype) {
-  if (!(astype == MC_I2 || astype == MC_U2 || astype == MC_I4 || astype == MC_U4)) return 0;
-  return mc_scan1p_enabled() ? mc_c4_dec1p_state_bytes(n, astype) : 0;
-}
-
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n) {
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  const size_t three = 24 * ((ntiles + 1) / 2);  // pair totals, first values, pair prefixes
-  const size_t one = mc_c4_dec1p_state_bytes(n, MC_I4);  // the larger of the two state sizes
-  return three > one ? three : one;
-}
-
-int mc_fso_delta_shuffle_decode_state(const void *src, void *dst, size_t n, int astype, int dtype,
-                                      double scale, double offset, void *state, size_t state_bytes,
-                                      void *workspace, size_t workspace_bytes, mc_stream_t stream) {
-  if (n == 0) return MC_OK;
-  if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
-  const size_t sb = mc_fso_delta_shuffle_decode_state_bytes(n, astype);
-  if (sb && state && (uintptr_t)state % 16 == 0 && state_bytes >= sb)
-    return mc_c4_dec1p(src, dst, n, astype, dtype, scale, offset, state, (hipStream_t)stream);
-  return mc_fso_delta_shuffle_decode(src, dst, n, astype, dtype, scale, offset, workspace, workspace_bytes,
-                                     stream);
+  return 24 * ((ntiles + 1) / 2);  // pair totals, first values, pair prefixes
 }
 
 int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype, int dtype,
                                 double scale, double offset, void *workspace,
                                 size_t workspace_bytes, mc_stream_t stream) {
-  if (n == 0) return MC_OK;
-  if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
-  if (!workspace || workspace_bytes < mc_fso_delta_shuffle_decode_workspace(n)) return MC_ENOSPC;
-  hipStream_t st = (hipStream_t)stream;
-  const size_t sb = mc_fso_delta_shuffle_decode_state_bytes(n, astype);
-  if (sb && (uintptr_t)workspace % 16 == 0) {
-    // single pass; the workspace's leading state bytes are zeroed here (the
-    // _state entry point keeps them zeroed across calls and skips this)
-    const int rc = mc_hip_status(hipMemsetAsync(workspace, 0, sb, st));
-    if (rc != MC_OK) return rc;
-    return mc_c4_dec1p(src, dst, n, astype, dtype, scale, offset, workspace, st);
-  }
-  return mc_c4_decode_three_pass(src, dst, n, astype, dtype, scale, offset, workspace, workspace_bytes, stream);
-}
-
-}  // extern "C"
-
-// The three-pass decode (tile totals, scan of the totals, rescan + FSO
-// decode): the schedule before the single-pass one, kept as the fallback for
-// an unaligned workspace and MCODEC_SCAN1P=0, and for the lab's A/B.
-int mc_c4_decode_three_pass(const void *src, void *dst, size_t n, int astype, int dtype, double scale,
-                            double offset, void *workspace, size_t workspace_bytes, mc_stream_t stream) {
   if (n == 0) return MC_OK;
   if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
   if (!workspace || workspace_bytes < mc_fso_delta_shuffle_decode_workspace(n)) return MC_ENOSPC;
@@ -235,3 +185,5 @@ int mc_c4_decode_three_pass(const void *src, void *dst, size_t n, int astype, in
   MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
   return mc_last_launch();
 }
+
+}  // extern "C"

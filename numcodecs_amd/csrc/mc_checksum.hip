@@ -194,6 +194,117 @@ MC_DEV uint64_t wave_sum(uint64_t v) {
   return v;
 }
 
+MC_DEV uint32_t load_le32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+MC_DEV void store_le32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+  p[3] = (uint8_t)(v >> 24);
+}
+
+// Powers of x the CRC finalize needs, the same for every chunk of a call:
+// computed once on the host (a device thread raising x to a 2^25 power with
+// bit-serial products took ~7 us of serial time per call).
+struct CrcFin {
+  uint32_t xb[32];          // X * (bit m): basis of the product by X = x^(8 * tile bytes)
+  uint32_t tail[MC_BLOCK];  // X^(tiles - hi(t)): moves thread t's fold to the chunk end
+  uint32_t pad;             // x^(-8 * zero padding of the last tile)
+  uint32_t xn;              // x^(8 * chunk bytes)
+};
+
+// tile partial words: plain, or agent-scope relaxed atomics (sc1) for the
+// in-launch hand-off to the last block (MI355X_MICROARCH.md, Valid forms,
+// table row 1)
+template <bool SC1>
+MC_DEV uint32_t ck_ld(const uint32_t *p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+// Fold chunk c's tile partials into the checksum (every thread of the
+// block); write it to out[c] (if out) and/or as a little-endian footer at
+// footer + c*footer_stride, and the stored footer to stored_out[c].
+// (`out` / `stored_out` may be host-mapped pinned memory.)
+template <int KIND, int K, bool SC1>
+MC_DEV void ck_finish_chunk(const CrcFin &fin, const uint32_t *partials, size_t tiles_per_chunk, size_t n,
+                            uint32_t init, uint32_t *out, uint8_t *footer, size_t footer_stride,
+                            const uint8_t *stored, size_t stored_stride, uint32_t *stored_out, size_t c) {
+  __shared__ uint64_t red[2][MC_BLOCK / 64];
+  if (stored_out && threadIdx.x == 0) stored_out[c] = load_le32(stored + c * stored_stride);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t lo = tiles_per_chunk * threadIdx.x / MC_BLOCK;
+  const size_t hi = tiles_per_chunk * (threadIdx.x + 1) / MC_BLOCK;
+  uint32_t result;
+  if constexpr (KIND == K_ADLER) {
+    uint64_t s1 = 0, s2 = 0;
+    for (size_t j = lo; j < hi; ++j) {
+      s1 += ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j)]);
+      s2 += ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j) + 1]);
+    }
+    s1 = wave_sum(s1 % ADLER_P);
+    s2 = wave_sum(s2 % ADLER_P);
+    if (lane == 0) {
+      red[0][wave] = s1;
+      red[1][wave] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint64_t x = 0, y = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) {
+      x += red[0][w];
+      y += red[1][w];
+    }
+    // zlib.adler32(data, value): a0 = value & 0xffff, b0 = value >> 16
+    const uint64_t a0 = init & 0xffffu, b0 = init >> 16;
+    const uint64_t a = (a0 + x) % ADLER_P;
+    const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
+    result = (uint32_t)((b << 16) | a);
+  } else {
+    // Horner over this thread's tiles; the product by the constant X is
+    // linear in the bits of acc: 4 byte tables in LDS built from X's basis
+    __shared__ uint32_t T[4][256];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((threadIdx.x >> k) & 1) r ^= fin.xb[8 * j + k];
+      T[j][threadIdx.x] = r;
+    }
+    __syncthreads();
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (size_t j = lo; j < hi; ++j)
+      acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
+            ck_ld<SC1>(&partials[c * tiles_per_chunk + j]);
+    if (hi > lo) acc = gf_mul(acc, fin.tail[threadIdx.x], crc_poly<KIND>());
+    acc = wave_xor(acc);
+    if (lane == 0) red[0][wave] = acc;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint32_t r = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
+    // r covers tiles_per_chunk * TB bytes; the last (TB*tiles - n) are padding
+    r = gf_mul(r, fin.pad, crc_poly<KIND>());
+    // crc(D, value) = ~raw(~value, D) = ~(~value * x^(8n) xor raw(0, D))
+    result = ~(gf_mul(~init, fin.xn, crc_poly<KIND>()) ^ r);
+  }
+  if (out) out[c] = result;
+  if (footer) store_le32(footer + c * footer_stride, result);
+}
+
+template <int KIND, int K>
+__global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
+    const CrcFin fin, const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
+    uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride,
+    const uint8_t *__restrict__ stored, size_t stored_stride, uint32_t *__restrict__ stored_out) {
+  ck_finish_chunk<KIND, K, false>(fin, partials, tiles_per_chunk, n, init, out, footer, footer_stride, stored,
+                                  stored_stride, stored_out, blockIdx.x);
+}
+
 // ---------------------------------------------------------------------------
 // Per-tile partials.  Block loops over tiles (tile = chunk * tiles_per_chunk
 // + t); the CRC tables are staged into LDS once per block.
@@ -201,11 +312,23 @@ MC_DEV uint64_t wave_sum(uint64_t v) {
 //   Adler: partials[2*tile] = S1 mod P, partials[2*tile+1] = S2 mod P
 // COPY: also write the payload to dst (+ per-row offset already applied).
 // ---------------------------------------------------------------------------
-template <int KIND, int K, bool COPY, int ALS, int ALD>
+// FUSED (one chunk): partials are stored sc1 and every block arrives
+// (mc_arrive_last, sharded counter) after a vmcnt(0) wait; the last block
+// folds them in the same launch (ck_finish_chunk) and zeroes the counter
+// again -- one launch, no finalize boundary.
+struct CkFinish {
+  uint32_t init;
+  uint32_t *ticket, *out, *stored_out;
+  uint8_t *footer;
+  size_t footer_stride;
+  const uint8_t *stored;
+};
+
+template <int KIND, int K, bool COPY, int ALS, int ALD, bool FUSED>
 __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t n, size_t tiles_per_chunk, size_t total_tiles,
-    uint32_t *__restrict__ partials) {
+    uint32_t *__restrict__ partials, const CrcFin fin, const CkFinish fx) {
   constexpr bool CRC = KIND != K_ADLER;
   __shared__ uint32_t V[CRC ? 16 * 256 : 1];
   __shared__ uint64_t red[2][MC_BLOCK / 64];
@@ -248,7 +371,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
       if (threadIdx.x == 0) {
         uint32_t r = 0;
         for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
-        partials[tile] = r;
+        if constexpr (FUSED) __hip_atomic_store(&partials[tile], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else partials[tile] = r;
       }
     } else {
       uint64_t s1 = 0, s2a = 0, s2b = 0;
@@ -284,105 +408,30 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
           x += red[0][w];
           y += red[1][w];
         }
-        partials[2 * tile] = (uint32_t)(x % ADLER_P);
-        partials[2 * tile + 1] = (uint32_t)(y % ADLER_P);
+        if constexpr (FUSED) {
+          __hip_atomic_store(&partials[2 * tile], (uint32_t)(x % ADLER_P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&partials[2 * tile + 1], (uint32_t)(y % ADLER_P), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          partials[2 * tile] = (uint32_t)(x % ADLER_P);
+          partials[2 * tile + 1] = (uint32_t)(y % ADLER_P);
+        }
       }
     }
     __syncthreads();  // red[] is reused by the next tile
   }
-}
-
-MC_DEV uint32_t load_le32(const uint8_t *p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-MC_DEV void store_le32(uint8_t *p, uint32_t v) {
-  p[0] = (uint8_t)v;
-  p[1] = (uint8_t)(v >> 8);
-  p[2] = (uint8_t)(v >> 16);
-  p[3] = (uint8_t)(v >> 24);
-}
-
-// Powers of x the CRC finalize needs, the same for every chunk of a call:
-// computed once on the host (a device thread raising x to a 2^25 power with
-// bit-serial products took ~7 us of serial time per call).
-struct CrcFin {
-  uint32_t xb[32];          // X * (bit m): basis of the product by X = x^(8 * tile bytes)
-  uint32_t tail[MC_BLOCK];  // X^(tiles - hi(t)): moves thread t's fold to the chunk end
-  uint32_t pad;             // x^(-8 * zero padding of the last tile)
-  uint32_t xn;              // x^(8 * chunk bytes)
-};
-
-// One block per chunk: fold the tile partials into the checksum; write it to
-// out[c] (if out) and/or as a little-endian footer at footer + c*footer_stride.
-template <int KIND, int K>
-__global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
-    const CrcFin fin, const uint32_t *__restrict__ partials, size_t tiles_per_chunk, size_t n, uint32_t init,
-    uint32_t *__restrict__ out, uint8_t *__restrict__ footer, size_t footer_stride,
-    const uint8_t *__restrict__ stored, size_t stored_stride, uint32_t *__restrict__ stored_out) {
-  __shared__ uint64_t red[2][MC_BLOCK / 64];
-  const size_t c = blockIdx.x;
-  if (stored_out && threadIdx.x == 0) stored_out[c] = load_le32(stored + c * stored_stride);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t lo = tiles_per_chunk * threadIdx.x / MC_BLOCK;
-  const size_t hi = tiles_per_chunk * (threadIdx.x + 1) / MC_BLOCK;
-  uint32_t result;
-  if constexpr (KIND == K_ADLER) {
-    uint64_t s1 = 0, s2 = 0;
-    for (size_t j = lo; j < hi; ++j) {
-      s1 += partials[2 * (c * tiles_per_chunk + j)];
-      s2 += partials[2 * (c * tiles_per_chunk + j) + 1];
-    }
-    s1 = wave_sum(s1 % ADLER_P);
-    s2 = wave_sum(s2 % ADLER_P);
-    if (lane == 0) {
-      red[0][wave] = s1;
-      red[1][wave] = s2;
+  if constexpr (FUSED) {
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0) {  // every block has at least one tile (grid <= tiles)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = mc_arrive_last(fx.ticket, gridDim.x);
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    uint64_t x = 0, y = 0;
-    for (int w = 0; w < MC_BLOCK / 64; ++w) {
-      x += red[0][w];
-      y += red[1][w];
-    }
-    // zlib.adler32(data, value): a0 = value & 0xffff, b0 = value >> 16
-    const uint64_t a0 = init & 0xffffu, b0 = init >> 16;
-    const uint64_t a = (a0 + x) % ADLER_P;
-    const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
-    result = (uint32_t)((b << 16) | a);
-  } else {
-    // Horner over this thread's tiles; the product by the constant X is
-    // linear in the bits of acc: 4 byte tables in LDS built from X's basis
-    __shared__ uint32_t T[4][256];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if ((threadIdx.x >> k) & 1) r ^= fin.xb[8 * j + k];
-      T[j][threadIdx.x] = r;
-    }
-    __syncthreads();
-    uint32_t acc = 0;
-#pragma unroll 4
-    for (size_t j = lo; j < hi; ++j)
-      acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
-            partials[c * tiles_per_chunk + j];
-    if (hi > lo) acc = gf_mul(acc, fin.tail[threadIdx.x], crc_poly<KIND>());
-    acc = wave_xor(acc);
-    if (lane == 0) red[0][wave] = acc;
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    uint32_t r = 0;
-    for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= (uint32_t)red[0][w];
-    // r covers tiles_per_chunk * TB bytes; the last (TB*tiles - n) are padding
-    r = gf_mul(r, fin.pad, crc_poly<KIND>());
-    // crc(D, value) = ~raw(~value, D) = ~(~value * x^(8n) xor raw(0, D))
-    result = ~(gf_mul(~init, fin.xn, crc_poly<KIND>()) ^ r);
+    if (!last) return;
+    ck_finish_chunk<KIND, K, true>(fin, partials, tiles_per_chunk, n, fx.init, fx.out, fx.footer,
+                                   fx.footer_stride, fx.stored, src_stride, fx.stored_out, 0);
+    if (threadIdx.x == 0) mc_arrivals_reset(fx.ticket);  // left zero for the next launch
   }
-  if (out) out[c] = result;
-  if (footer) store_le32(footer + c * footer_stride, result);
 }
 
 // ---------------------------------------------------------------------------
@@ -563,29 +612,37 @@ inline int align_class(const void *p, size_t stride, size_t nchunks) {
 
 template <int KIND, int K, bool COPY, int ALS, int ALD>
 void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
-                  size_t total, uint32_t *parts, hipStream_t st) {
+                  size_t total, uint32_t *parts, const CrcFin &fin, const CkFinish *fx, hipStream_t st) {
   const unsigned cap = ck_grid_cap(COPY);
   const unsigned grid = (unsigned)(total < cap ? total : cap);
-  k_ck_tiles<KIND, K, COPY, ALS, ALD><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts);
+  if constexpr (!COPY && ALS == ALD) {  // the fused finish serves the verify (no copy) only
+    if (fx) {
+      k_ck_tiles<KIND, K, COPY, ALS, ALD, true><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts,
+                                                                           fin, *fx);
+      return;
+    }
+  }
+  k_ck_tiles<KIND, K, COPY, ALS, ALD, false><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts, fin,
+                                                                        CkFinish{});
 }
 
 template <int KIND, int K>
 void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
-                    size_t tpc, uint32_t *parts, hipStream_t st) {
+                    size_t tpc, uint32_t *parts, const CrcFin &fin, const CkFinish *fx, hipStream_t st) {
   const size_t total = tpc * nchunks;
   const int als = align_class(s, ss, nchunks);
   if (!d) {
-    if (als == 2) launch_tiles<KIND, K, false, 2, 2>(s, ss, d, ds, n, tpc, total, parts, st);
-    else if (als == 1) launch_tiles<KIND, K, false, 1, 1>(s, ss, d, ds, n, tpc, total, parts, st);
-    else launch_tiles<KIND, K, false, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
+    if (als == 2) launch_tiles<KIND, K, false, 2, 2>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+    else if (als == 1) launch_tiles<KIND, K, false, 1, 1>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+    else launch_tiles<KIND, K, false, 0, 0>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
     return;
   }
   const int ald = align_class(d, ds, nchunks);
-  if (als == 2 && ald == 2) launch_tiles<KIND, K, true, 2, 2>(s, ss, d, ds, n, tpc, total, parts, st);
-  else if (als == 1 && ald == 2) launch_tiles<KIND, K, true, 1, 2>(s, ss, d, ds, n, tpc, total, parts, st);
-  else if (als == 2 && ald == 1) launch_tiles<KIND, K, true, 2, 1>(s, ss, d, ds, n, tpc, total, parts, st);
-  else if (als >= 1 && ald >= 1) launch_tiles<KIND, K, true, 1, 1>(s, ss, d, ds, n, tpc, total, parts, st);
-  else launch_tiles<KIND, K, true, 0, 0>(s, ss, d, ds, n, tpc, total, parts, st);
+  if (als == 2 && ald == 2) launch_tiles<KIND, K, true, 2, 2>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+  else if (als == 1 && ald == 2) launch_tiles<KIND, K, true, 1, 2>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+  else if (als == 2 && ald == 1) launch_tiles<KIND, K, true, 2, 1>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+  else if (als >= 1 && ald >= 1) launch_tiles<KIND, K, true, 1, 1>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
+  else launch_tiles<KIND, K, true, 0, 0>(s, ss, d, ds, n, tpc, total, parts, fin, fx, st);
 }
 
 // host: x^(2^k) / x^(-2^k) tables (64 squarings, once per polynomial)
@@ -660,19 +717,26 @@ const CrcFin &crc_fin(int K, size_t tpc, size_t n) {
 template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
                   uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
-                  uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st) {
+                  uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st, uint32_t *ticket) {
   const int K = ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;
   uint32_t *parts = static_cast<uint32_t *>(ws);
+  // one chunk, no copy, with a ticket: finish in the tiles launch
+  // (ck_finish_chunk)
+  const bool fused = ticket && nchunks == 1 && !d;
+  const CkFinish fx{init, ticket, out, stored_out, footer, fs, stored};
   switch (K) {
 #define MC_CK_CASE(KK)                                                                         \
-  case KK:                                                                                     \
-    dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, st);                        \
-    k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                           \
-        crc_fin<KIND>(KK, tpc, n), parts, tpc, n, init, out, footer, fs, stored, ss, stored_out); \
-    break;
+  case KK: {                                                                                   \
+    const CrcFin &fin = crc_fin<KIND>(KK, tpc, n);                                             \
+    dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, fin, fused ? &fx : nullptr, st); \
+    if (!fused)                                                                                \
+      k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                         \
+          fin, parts, tpc, n, init, out, footer, fs, stored, ss, stored_out);                  \
+    break;                                                                                     \
+  }
     MC_CK_CASE(1)
     MC_CK_CASE(4)
     MC_CK_CASE(8)
@@ -687,17 +751,17 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
 int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks,
                 size_t n, uint32_t init, const uint8_t *prefix, size_t plen, uint32_t *out,
                 uint8_t *footer, size_t fs, const uint8_t *stored, uint32_t *stored_out, void *ws,
-                size_t ws_bytes, hipStream_t st) {
+                size_t ws_bytes, hipStream_t st, uint32_t *ticket = nullptr) {
   switch (kind) {
     case MC_CK_CRC32:
       return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st);
+                                    ws, ws_bytes, st, ticket);
     case MC_CK_CRC32C:
       return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                     ws, ws_bytes, st);
+                                     ws, ws_bytes, st, ticket);
     case MC_CK_ADLER32:
       return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st);
+                                    ws, ws_bytes, st, ticket);
     case MC_CK_JENKINS: {
       if (d && n) {
         const int rc = mc_copy_rows_impl(s, ss, d, ds, n, nchunks, st);
@@ -778,6 +842,28 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride, voi
   return ck_dispatch(kind, payload, src_stride, static_cast<uint8_t *>(dst), dst_stride, nchunks, n,
                      init, static_cast<const uint8_t *>(prefix), prefix_bytes, out_sums, nullptr, 0,
                      stored, out_stored, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+// Checksum32.decode's verification of ONE encoded buffer in one launch: the
+// checksum's last tile block folds the partials (CRC32 / CRC32C / Adler32;
+// Jenkins is one kernel anyway).  out_pair[0] = checksum of the payload,
+// out_pair[1] = the stored LE32 value; out_pair may be host-mapped pinned
+// memory.  `ticket`: one device word, zero before the first call, left zero
+// (keep one per stream); NULL = the two-launch path.
+int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, uint32_t init,
+                               const void *prefix, size_t prefix_bytes, int location, uint32_t *out_pair,
+                               void *workspace, size_t workspace_bytes, uint32_t *ticket,
+                               mc_stream_t stream) {
+  if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
+  if (encoded_bytes < 4 || !src || !out_pair) return MC_EINVAL;
+  if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
+  const size_t n = encoded_bytes - 4;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  const uint8_t *payload = location == MC_CK_START ? s + 4 : s;
+  const uint8_t *stored = location == MC_CK_START ? s : s + n;
+  return ck_dispatch(kind, payload, encoded_bytes, nullptr, 0, 1, n, init, static_cast<const uint8_t *>(prefix),
+                     prefix_bytes, out_pair, nullptr, 0, stored, out_pair + 1, workspace, workspace_bytes,
+                     (hipStream_t)stream, ticket);
 }
 
 }  // extern "C"

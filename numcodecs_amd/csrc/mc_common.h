@@ -74,6 +74,33 @@ int mc_copy_rows_impl(const void *src, size_t src_stride, void *dst, size_t dst_
 
 static constexpr int MC_BLOCK = 256;  // 4 waves of 64 lanes
 
+// ---------------------------------------------------------------------------
+// "Last block arrives" for an in-launch finish (no finalize kernel): an
+// arrival counter sharded 8 ways (tickets[0..7], block b counts in shard
+// b % 8, as blocks are dealt round-robin over the 8 XCDs) plus
+// tickets[8] = shards completed.  One word alone saturates at ~88 atomics/us
+// (MI355X_MICROARCH.md, "dequeue"/"fanin"): 8192 arrivals on it took ~90 us.
+// Called by thread 0 of every block, after the block's hand-off stores and an
+// `s_waitcnt vmcnt(0)`; true in exactly one block -- the last -- which then
+// finishes and calls mc_arrivals_reset (every other arrival is done by then,
+// so the words are left zero for the next launch).  MC_ARRIVAL_WORDS words,
+// zero before the first launch.
+// ---------------------------------------------------------------------------
+static constexpr int MC_ARRIVAL_WORDS = 16;
+
+__device__ inline bool mc_arrive_last(uint32_t *tickets, unsigned nblocks) {
+  const unsigned s = blockIdx.x & 7u;
+  const unsigned nshards = nblocks < 8u ? nblocks : 8u;
+  const unsigned per = (nblocks - s + 7u) / 8u;  // blocks b < nblocks with b % 8 == s
+  if (atomicAdd(&tickets[s], 1u) != per - 1u) return false;
+  return atomicAdd(&tickets[8], 1u) == nshards - 1u;
+}
+
+__device__ inline void mc_arrivals_reset(uint32_t *tickets) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) tickets[i] = 0;
+}
+
 // grid cap for grid-stride streaming kernels: 256 CUs x 8 blocks of 256 threads
 static constexpr unsigned MC_MAX_GRID = 256u * 8u;
 

@@ -137,20 +137,51 @@ MC_DEV void f32_st(uint8_t *p, mc_u32x4 v) {
 // block = (chunk c, slice sl); partials[block] = {S1, S2, nz}
 // AL: alignment class of src/dst rows (above); 0 = bytes only
 // ---------------------------------------------------------------------------
+enum FinalMode { F_SUM = 0, F_FOOTER = 1, F_VERIFY = 2 };
+
+// partial words of a (chunk, slice) block: plain, or agent-scope relaxed
+// atomics (global_load/store ... sc1) for the in-launch hand-off to the last
+// block of a chunk (MI355X_MICROARCH.md, Valid forms, table row 1: one lane
+// per storing workgroup stores sc1, waits vmcnt(0), adds to ONE counter; the
+// workgroup whose add came last loads sc1 after a barrier)
+template <bool SC1>
+MC_DEV uint32_t part_ld(const uint32_t *p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+// Fold chunk c's slice partials and finish it (every thread of the block):
+//   F_SUM:    out[c] = checksum
+//   F_FOOTER: LE32 checksum at dst + c*dst_stride + nbytes (and out[c] if set)
+//   F_VERIFY: out[2c] = checksum, out[2c+1] = LE32 footer at src + c*src_stride + nbytes
+// (`out` may be host-mapped pinned memory: the public decode reads its
+// verdict from there after one stream sync)
+template <bool SC1>
+MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t c, int mode,
+                             const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
+                             size_t nbytes, uint32_t *out);
+
+// block = (chunk c, slice sl), partials[block] = {S1, S2, nz}; or, with
+// `tickets` (one chunk, FUSED finish): a persistent grid, block b sums slices
+// b, b + grid, ... (absolute weights: slice partials add), stores ONE partial
+// sc1, arrives (mc_arrive_last) and the last block folds the grid's partials
+// and finishes the chunk in this launch
 template <bool COPY, int AL, int F32_UNROLL, bool NT>
 __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
-    size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials) {
-  const size_t c = blockIdx.x / nslices;
-  const unsigned sl = blockIdx.x - (unsigned)(c * nslices);
+    size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials,
+    uint32_t *tickets, int mode, uint32_t *out) {
+  const size_t c = tickets ? 0 : blockIdx.x / nslices;
+  const unsigned sl0 = tickets ? blockIdx.x : blockIdx.x - (unsigned)(c * nslices);
+  const unsigned sl_step = tickets ? gridDim.x : nslices;
   const uint8_t *s = src + c * src_stride;
   uint8_t *d = COPY ? dst + c * dst_stride : nullptr;
   const uint64_t nwords = (nbytes + 1) / 2;
   const size_t nvec = AL ? nbytes / 16 : 0;
-  const size_t v_lo = nvec * sl / nslices, v_hi = nvec * (sl + 1) / nslices;
   F32Part p;
   part_init(p);
-  {
+  for (unsigned sl = sl0; sl < nslices; sl += sl_step) {
+    const size_t v_lo = nvec * sl / nslices, v_hi = nvec * (sl + 1) / nslices;
     size_t v = v_lo + threadIdx.x;
     // weight of the vector's first word, stepped by 8*MC_BLOCK words per iteration
     uint32_t cw = (uint32_t)((nwords - 8 * (uint64_t)v) % M);
@@ -173,49 +204,58 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
       part_vec(p, x, cw);
       cw = cw >= STEP ? cw - STEP : cw + M - STEP;
     }
-  }
-  if (sl == nslices - 1) {  // bytes after the last whole vector, word by word
-    const size_t b0 = nvec * 16;
-    for (size_t b = b0 + 2 * (size_t)threadIdx.x; b < nbytes; b += 2 * MC_BLOCK) {
-      const uint32_t hi = s[b];
-      const uint32_t lo = b + 1 < nbytes ? s[b + 1] : 0u;
-      if constexpr (COPY) {
-        d[b] = (uint8_t)hi;
-        if (b + 1 < nbytes) d[b + 1] = (uint8_t)lo;
+    if (sl == nslices - 1) {  // bytes after the last whole vector, word by word
+      const size_t b0 = nvec * 16;
+      for (size_t b = b0 + 2 * (size_t)threadIdx.x; b < nbytes; b += 2 * MC_BLOCK) {
+        const uint32_t hi = s[b];
+        const uint32_t lo = b + 1 < nbytes ? s[b + 1] : 0u;
+        if constexpr (COPY) {
+          d[b] = (uint8_t)hi;
+          if (b + 1 < nbytes) d[b + 1] = (uint8_t)lo;
+        }
+        part_word(p, (hi << 8) | lo, (uint32_t)((nwords - b / 2) % M));
       }
-      part_word(p, (hi << 8) | lo, (uint32_t)((nwords - b / 2) % M));
     }
   }
   uint32_t s1, s2, nz;
   block_reduce(p, s1, s2, nz);
-  if (threadIdx.x == 0) {
-    partials[3 * (size_t)blockIdx.x + 0] = s1;
-    partials[3 * (size_t)blockIdx.x + 1] = s2;
-    partials[3 * (size_t)blockIdx.x + 2] = nz;
+  if (!tickets) {  // a separate finalize launch folds the partials
+    if (threadIdx.x == 0) {
+      partials[3 * (size_t)blockIdx.x + 0] = s1;
+      partials[3 * (size_t)blockIdx.x + 1] = s2;
+      partials[3 * (size_t)blockIdx.x + 2] = nz;
+    }
+    return;
   }
+  // fused finish: the last block to arrive folds the grid's partials in this
+  // launch (no finalize kernel, no extra boundary)
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) {
+    uint32_t *q = partials + 3 * (size_t)blockIdx.x;
+    __hip_atomic_store(q + 0, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = mc_arrive_last(tickets, gridDim.x);
+  }
+  __syncthreads();
+  if (!last) return;
+  f32_finish_chunk<true>(partials, gridDim.x, 0, mode, src, src_stride, dst, dst_stride, nbytes, out);
+  if (threadIdx.x == 0) mc_arrivals_reset(tickets);
 }
 
-enum FinalMode { F_SUM = 0, F_FOOTER = 1, F_VERIFY = 2 };
-
-// one workgroup per chunk: the 256 threads fold the chunk's slices (a large
-// chunk has thousands: a single thread walking them serially was the
-// bottleneck of a 256 MiB checksum), then
-//   F_SUM:    out[c] = checksum
-//   F_FOOTER: LE32 checksum at dst + c*dst_stride + nbytes (and out[c] if set)
-//   F_VERIFY: out[2c] = checksum, out[2c+1] = LE32 footer at src + c*src_stride + nbytes
-__global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
-    const uint32_t *__restrict__ partials, unsigned nslices, size_t nchunks, int mode,
-    const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
-    size_t dst_stride, size_t nbytes, uint32_t *__restrict__ out) {
-  const size_t c = blockIdx.x;
+template <bool SC1>
+MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t c, int mode,
+                             const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
+                             size_t nbytes, uint32_t *out) {
   F32Part p;
   part_init(p);
 #pragma unroll 8
   for (unsigned sl = threadIdx.x; sl < nslices; sl += MC_BLOCK) {
     const uint32_t *q = partials + 3 * (c * nslices + sl);
-    p.s1 += q[0];
-    p.s2a += q[1];  // partial S2 already reduced: s2b stays 0
-    p.nz |= q[2];
+    p.s1 += part_ld<SC1>(q);
+    p.s2a += part_ld<SC1>(q + 1);  // partial S2 already reduced: s2b stays 0
+    p.nz |= part_ld<SC1>(q + 2);
   }
   uint32_t a, b, z;
   block_reduce(p, a, b, z);
@@ -230,6 +270,17 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
     out[2 * c] = f;
     out[2 * c + 1] = load_le32(src + c * src_stride + nbytes);
   }
+}
+
+// one workgroup per chunk: the 256 threads fold the chunk's slices (a large
+// chunk has thousands: a single thread walking them serially was the
+// bottleneck of a 256 MiB checksum) -- f32_finish_chunk
+__global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
+    const uint32_t *__restrict__ partials, unsigned nslices, size_t nchunks, int mode,
+    const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
+    size_t dst_stride, size_t nbytes, uint32_t *__restrict__ out) {
+  (void)nchunks;
+  f32_finish_chunk<false>(partials, nslices, blockIdx.x, mode, src, src_stride, dst, dst_stride, nbytes, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -376,23 +427,25 @@ static int align_class(const void *p, size_t stride, size_t nchunks) {
 
 static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                            size_t nchunks, size_t nbytes, unsigned nsl, uint32_t *partials,
-                           hipStream_t st) {
+                           uint32_t *tickets, int mode, uint32_t *out, hipStream_t st) {
   int al = align_class(src, src_stride, nchunks);
   if (dst) {
     const int ad = align_class(dst, dst_stride, nchunks);
     al = al < ad ? al : ad;
   }
-  const unsigned grid = (unsigned)(nchunks * nsl);
+  // fused (one chunk): a persistent grid of at most 1024 blocks, so that the
+  // last block folds at most 1024 partials
+  const unsigned grid = tickets ? (nsl < 1024u ? nsl : 1024u) : (unsigned)(nchunks * nsl);
 #define MC_F32_U(CP, AL, U)                                                                   \
   do {                                                                                         \
     if (f32_ntld())                                                                            \
       k_f32_partial<CP, AL, U, true><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,          \
                                                                 dst_stride, nbytes, nsl,       \
-                                                                partials);                     \
+                                                                partials, tickets, mode, out); \
     else                                                                                       \
       k_f32_partial<CP, AL, U, false><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,         \
                                                                  dst_stride, nbytes, nsl,      \
-                                                                 partials);                    \
+                                                                 partials, tickets, mode, out);\
   } while (0)
 #define MC_F32_LAUNCH(CP, AL)                                                                 \
   do {                                                                                         \
@@ -413,19 +466,22 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
 #undef MC_F32_U
 }
 
-// standalone driver: checksum (+ optional copy) of nchunks chunks, then finalize
+// standalone driver: checksum (+ optional copy) of nchunks chunks, then
+// finalize -- in the same launch when `tickets` (MC_ARRIVAL_WORDS zeroed
+// words, left zeroed; one chunk only) is given, else as a second launch
 static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                    size_t nchunks, size_t nbytes, int mode, uint32_t *out, void *ws,
-                   size_t ws_bytes, hipStream_t st) {
+                   size_t ws_bytes, hipStream_t st, uint32_t *tickets = nullptr) {
   const unsigned nsl = slices_for(nbytes, nchunks);
   if (!ws || ws_bytes < partials_bytes(nchunks, nsl)) return MC_ENOSPC;
   uint32_t *partials = static_cast<uint32_t *>(ws);
   // F_FOOTER copies the payload in front of its footer; F_VERIFY with a dst
   // compacts the payloads out of the encoded rows (the decode pass)
   const bool copy = dst != nullptr;
-  launch_partial(src, src_stride, copy ? dst : nullptr, dst_stride, nchunks, nbytes, nsl, partials, st);
+  launch_partial(src, src_stride, copy ? dst : nullptr, dst_stride, nchunks, nbytes, nsl, partials, tickets, mode,
+                 out, st);
   int rc = mc_last_launch();
-  if (rc != MC_OK) return rc;
+  if (rc != MC_OK || tickets) return rc;
   k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride,
                                                          dst, dst_stride, nbytes, out);
   return mc_last_launch();
@@ -480,6 +536,15 @@ int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair, voi
   const size_t payload = nbytes - 4;  // payload 0: checksum 0, footer still read
   return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, payload, F_VERIFY, out_pair,
                  workspace, workspace_bytes, st);
+}
+
+int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_pair, void *workspace,
+                               size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
+  if (!ticket) return mc_fletcher32_verify(src, nbytes, out_pair, workspace, workspace_bytes, stream);
+  if ((uintptr_t)ticket % 4) return MC_EINVAL;
+  if (!src || !out_pair || nbytes < 4) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, nbytes - 4, F_VERIFY, out_pair, workspace,
+                 workspace_bytes, (hipStream_t)stream, ticket);
 }
 
 int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks, size_t chunk_bytes,
@@ -554,7 +619,7 @@ int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void 
     if (rc != MC_OK) return rc;
     const unsigned nsl = slices_for(chunk_bytes, nchunks);
     uint32_t *partials = static_cast<uint32_t *>(workspace);
-    launch_partial(d, dst_stride, nullptr, 0, nchunks, chunk_bytes, nsl, partials, st);
+    launch_partial(d, dst_stride, nullptr, 0, nchunks, chunk_bytes, nsl, partials, nullptr, F_SUM, nullptr, st);
     rc = mc_last_launch();
     if (rc != MC_OK) return rc;
     k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(

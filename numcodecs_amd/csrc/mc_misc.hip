@@ -13,6 +13,16 @@ const char *mc_strerror(int status) {
   return "unknown mcodec status";
 }
 
+int mc_stream_synchronize(mc_stream_t stream) {
+  return mc_hip_status(hipStreamSynchronize((hipStream_t)stream));
+}
+
+void *mc_host_device_pointer(void *host) {
+  void *d = nullptr;
+  if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  return d;
+}
+
 int mc_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -18,7 +18,6 @@
 //   * batches of chunks (mc_delta_decode_batch): one workgroup per chunk with
 //     a running carry (k_scan_rows), single pass.
 #include "mc_scan.h"
-#include "mc_lookback.h"
 
 #include <stdlib.h>
 
@@ -1102,57 +1101,13 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
                                size_t nchunks, size_t n, int astype, int dtype, int variant,
                                mc_stream_t stream);
 
-// single-pass same-width integer decode (mc_scan1p.hip)
-size_t mc_delta_dec1p_state_bytes(size_t n, int es);
-int mc_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, hipStream_t st,
-                   unsigned spins = MC_LB_WAVE_SPINS);
-
-// MCODEC_SCAN1P=0 selects the three-pass integer scans instead of the
-// single-pass ones (A/B measurement; both are bit-exact)
-bool mc_scan1p_enabled() {
-  static const bool b = [] {
-    const char *e = getenv("MCODEC_SCAN1P");
-    return !(e && atoi(e) == 0);
-  }();
-  return b;
-}
-
-namespace {
-// shapes the single-pass decode takes (alignment is checked per call)
-bool d1p_shape(size_t n, int astype, int dtype) {
-  if (astype != dtype || dtype == MC_B1 || mc_is_float(dtype)) return false;
-  const int es = mc_itemsize(dtype);
-  return (es == 1 || es == 2 || es == 4) && (n * (size_t)es) % 16 == 0 && mc_scan1p_enabled();
-}
-bool d1p_ok(const void *src, const void *dst, size_t n, int astype, int dtype) {
-  return d1p_shape(n, astype, dtype) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
-}
-}  // namespace
-
 extern "C" {
-
-size_t mc_delta_decode_state_bytes(size_t n, int astype, int dtype) {
-  if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype) || !d1p_shape(n, astype, dtype)) return 0;
-  return mc_delta_dec1p_state_bytes(n, mc_itemsize(dtype));
-}
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
   if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n, dtype) : 0;
   const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
   const size_t fast = astype == dtype && dtype != MC_B1 ? dscan_ws_entries(n, mc_itemsize(dtype)) : 0;
-  const size_t three = (generic > fast ? generic : fast) * sizeof(uint64_t);
-  const size_t one = mc_delta_decode_state_bytes(n, astype, dtype);
-  return three > one ? three : one;
-}
-
-int mc_delta_decode_state(const void *src, void *dst, size_t n, int astype, int dtype, void *state,
-                          size_t state_bytes, void *workspace, size_t workspace_bytes, mc_stream_t stream) {
-  if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
-  if (n == 0) return MC_OK;
-  if (state && (uintptr_t)state % 16 == 0 && d1p_ok(src, dst, n, astype, dtype) &&
-      state_bytes >= mc_delta_decode_state_bytes(n, astype, dtype))
-    return mc_delta_dec1p(src, dst, n, mc_itemsize(dtype), state, (hipStream_t)stream);
-  return mc_delta_decode(src, dst, n, astype, dtype, workspace, workspace_bytes, stream);
+  return (generic > fast ? generic : fast) * sizeof(uint64_t);
 }
 
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
@@ -1179,14 +1134,6 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
   }
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
   if (!workspace || workspace_bytes < mc_delta_decode_workspace(n, astype, dtype)) return MC_ENOSPC;
-  if (d1p_ok(src, dst, n, astype, dtype) && (uintptr_t)workspace % 16 == 0) {
-    // single pass; the workspace's leading state bytes are zeroed here (the
-    // _state entry point keeps them zeroed across calls and skips this)
-    const size_t sb = mc_delta_decode_state_bytes(n, astype, dtype);
-    const int rc = mc_hip_status(hipMemsetAsync(workspace, 0, sb, st));
-    if (rc != MC_OK) return rc;
-    return mc_delta_dec1p(src, dst, n, mc_itemsize(dtype), workspace, st);
-  }
   uint64_t *sums = static_cast<uint64_t *>(workspace);
   if (astype == dtype && dtype != MC_B1 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0 &&
       dscan_enabled()) {

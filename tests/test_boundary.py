@@ -147,7 +147,7 @@ def test_no_device_fails_loudly():
 def _header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*)\s*(mc_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*|void \*)\s*(mc_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_extern_c_and_plain_types():

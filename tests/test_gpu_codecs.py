@@ -517,3 +517,34 @@ def test_host_pipeline_roundtrip(device):
         assert np.array_equal(henc[c].numpy(), oracle.shuffle(xh[c], 4))
     batch.host_pipeline(henc, hdec, 4, False, slice_chunks=7)
     assert torch.equal(hdec, hin)
+
+
+@pytest.mark.parametrize("codec_id", ["fletcher32", "crc32", "crc32c", "adler32"])
+def test_single_chunk_verify_one_launch(device, codec_id):
+    """Decode of one device chunk verifies in ONE launch (the checksum's last
+    block folds the partials, fletcher32.pyx:91-115 / checksum32.py:72-88)
+    and reads its verdict from pinned host memory: sizes around the slice /
+    tile boundaries, repeated calls on the stream's ticket (left zero), a
+    second stream, and a corrupted byte raising the reference's error."""
+    from numcodecs_amd import CRC32, CRC32C, Adler32, _ops
+
+    make = {"fletcher32": Fletcher32, "crc32": CRC32, "crc32c": CRC32C, "adler32": Adler32}[codec_id]
+    for n in (1, 15, 16, 4096 * 8 - 3, 32768, 32769, 65536 * 3 + 7, (1 << 22) + 5):
+        x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=device)
+        enc = make().encode(x)
+        for _ in range(3):
+            assert torch.equal(make().decode(enc), x), (codec_id, n)
+        ref = oracle.fletcher32_encode(x.cpu().numpy()) if codec_id == "fletcher32" else \
+            oracle.checksum32_encode(codec_id, x.cpu().numpy()).tobytes()
+        assert enc.cpu().numpy().tobytes() == ref, (codec_id, n)
+        bad = enc.clone()
+        bad[n // 2 + (4 if codec_id != "fletcher32" and codec_id != "crc32c" else 0)] ^= 0x10
+        with pytest.raises(RuntimeError):
+            make().decode(bad)
+    side = torch.cuda.Stream(device)
+    with torch.cuda.stream(side):
+        y = torch.randint(0, 256, (100003,), dtype=torch.uint8, device=device)
+        assert torch.equal(make().decode(make().encode(y)), y)
+    torch.cuda.synchronize()
+    for sl in _ops._VERIFY.values():
+        assert not sl.ticket.any()

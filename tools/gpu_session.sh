@@ -2,7 +2,7 @@
 # Run a sequence of GPU steps on the box, each under its own time limit; stop
 # at the first step that crashes, aborts or times out (exit 124/134/137/139),
 # continue past ordinary test failures.  Usage: tools/gpu_session.sh STEP...
-# where STEP is one of: tests, smoke, bench, benchq, benchprof, pmcall, multi, probe, rocprof, pmc
+# where STEP is one of: tests, smoke, bench, benchq, benchprof, pmcall, multi, probe, t1p, p1p, prof1p, verify, rocprof, pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -29,8 +29,8 @@ for step in "$@"; do
     multi) run bench_multi2 600 env MCODEC_BENCH_BACKEND=gloo python bench.py --gpus 2 --no-cpu --quick --steps 50 --warmup 5 ;;
     probe) run probe_enc4 600 python tools/probe_enc.py 4 ;;
     t1p) run pytest_scan1p 600 python -u -m pytest tests/test_gpu_scan1p.py tests/test_gpu_c4.py tests/test_gpu_delta.py tests/test_gpu_fullsize.py -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf ;;
-    p1p) run probe_scan1p 300 python tools/probe_scan1p.py
-         run probe_scan3p 300 env MCODEC_SCAN1P=0 python tools/probe_scan1p.py ;;
+    p1p) run probe_scan1p 300 python tools/probe_scan1p.py ;;
+    verify) run probe_verify 300 python tools/probe_verify.py ;;
     prof1p) run rocprof_scan1p 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_scan1p -o scan -- python3 tools/probe_scan1p.py ;;
     rocprof) run rocprof_kt 600 rocprofv3 --kernel-trace --stats --output-format csv \
                -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --quick --steps 50 --warmup 5 ;;

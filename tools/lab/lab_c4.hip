@@ -4,8 +4,7 @@
 // FSO -> Delta -> Shuffle(2) chunk pipeline that DESIGN.md measured against
 // the product's 3-pass scan and rejected, kept so the measurement can be
 // repeated and so their byte-identity stays tested (tests/test_gpu_c4.py):
-//   1  the product's three-pass scan (its schedule before the single-pass
-//      partition scan of mc_scan1p.hip became the default)
+//   1  the product's three-pass scan (= 0)
 //   2  single-pass decoupled look-back, tiles numbered by an atomic counter
 //   3  single-pass look-back in workgroup (blockIdx) order
 //   4  = 3 with every wait replaced by the data-derived prefix fallback
@@ -217,10 +216,6 @@ static void c4_decode_lb(const uint8_t *s, uint8_t *d, uint8_t *ws, const C4Para
 
 }  // namespace
 
-// the product's schedules (mc_c4.hip): three-pass scan, and the default
-// (the single-pass partition scan of mc_scan1p.hip)
-int mc_c4_decode_three_pass(const void *src, void *dst, size_t n, int astype, int dtype, double scale,
-                            double offset, void *workspace, size_t workspace_bytes, mc_stream_t stream);
 
 extern "C" {
 
@@ -230,18 +225,16 @@ size_t mc_lab_c4_decode_workspace(size_t n) {
   return mc_lb_workspace(ntiles) > prod ? mc_lb_workspace(ntiles) : prod;
 }
 
-// variant 0: the product default (single pass, mc_scan1p.hip); 1: the
-// product's three-pass scan; 2-7 as listed above.  Identical bytes.
+// variant 0 / 1: the product's three-pass scan; 2-7 as listed above (the
+// partition-in-LDS single pass is mc_lab_c4_dec1p, lab_scan1p.hip).
+// Identical bytes.
 int mc_lab_c4_decode_variant(const void *src, void *dst, size_t n, int astype, int dtype, double scale,
                              double offset, void *workspace, size_t workspace_bytes, int variant,
                              mc_stream_t stream) {
   if (variant < 0 || variant > 7) return MC_EINVAL;
-  if (variant == 0)
+  if (variant <= 1)
     return mc_fso_delta_shuffle_decode(src, dst, n, astype, dtype, scale, offset, workspace, workspace_bytes,
                                        stream);
-  if (variant == 1)
-    return mc_c4_decode_three_pass(src, dst, n, astype, dtype, scale, offset, workspace, workspace_bytes,
-                                   stream);
   if (n == 0) return MC_OK;
   if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
   if (!workspace || workspace_bytes < mc_lab_c4_decode_workspace(n)) return MC_ENOSPC;

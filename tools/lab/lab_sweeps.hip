@@ -9,24 +9,33 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
                                size_t nchunks, size_t n, int astype, int dtype, int variant,
                                mc_stream_t stream);
 
-int mc_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, hipStream_t st, unsigned spins);
+size_t mc_delta_dec1p_state_bytes(size_t n, int es);
+size_t mc_c4_dec1p_state_bytes(size_t n, int astype);
+int mc_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, hipStream_t st, unsigned spins,
+                   uint64_t *trace);
 int mc_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype, double scale, double offset,
-                void *state, hipStream_t st, unsigned spins);
+                void *state, hipStream_t st, unsigned spins, uint64_t *trace);
 
 extern "C" {
 
-// The product's single-pass decodes (mc_scan1p.hip) with an explicit
-// look-back spin bound: 0 makes every partition whose predecessors have not
-// all published yet take the data-derived prefix (the guard path), so tests
-// can check that path byte for byte.  `state` as for mc_delta_decode_state.
+// The single-pass decodes (lab_scan1p.hip) with an explicit look-back spin
+// bound (MC_LB_WAVE_SPINS = 16384 normally; 0 makes every partition whose
+// predecessors have not all published yet take the data-derived prefix, the
+// guard path).  `state`: mc_lab_*_dec1p_state_bytes() device bytes, zero
+// before the first call, left zero by every call.
+// `trace` (may be NULL): 8 uint64 per partition, wall_clock64() at ticket,
+// staged, look-back resolved, emit start, emitted, and the workgroup id.
+size_t mc_lab_delta_dec1p_state_bytes(size_t n, int es) { return mc_delta_dec1p_state_bytes(n, es); }
+size_t mc_lab_c4_dec1p_state_bytes(size_t n, int astype) { return mc_c4_dec1p_state_bytes(n, astype); }
+
 int mc_lab_delta_dec1p(const void *src, void *dst, size_t n, int es, void *state, unsigned spins,
-                       mc_stream_t stream) {
-  return mc_delta_dec1p(src, dst, n, es, state, (hipStream_t)stream, spins);
+                       uint64_t *trace, mc_stream_t stream) {
+  return mc_delta_dec1p(src, dst, n, es, state, (hipStream_t)stream, spins, trace);
 }
 
 int mc_lab_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype, double scale, double offset,
-                    void *state, unsigned spins, mc_stream_t stream) {
-  return mc_c4_dec1p(src, dst, n, astype, dtype, scale, offset, state, (hipStream_t)stream, spins);
+                    void *state, unsigned spins, uint64_t *trace, mc_stream_t stream) {
+  return mc_c4_dec1p(src, dst, n, astype, dtype, scale, offset, state, (hipStream_t)stream, spins, trace);
 }
 
 // Shuffle with an explicit kernel layout and grid (mc_shuffle.hip Variant):

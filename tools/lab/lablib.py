@@ -18,8 +18,10 @@ _SIGS = {
     "mc_lab_delta_decode_batch_variant": ([_V, _S, _V, _S, _S, _S, _I, _I, _I, _V], _I),
     "mc_lab_c4_decode_workspace": ([_S], _S),
     "mc_lab_c4_decode_variant": ([_V, _V, _S, _I, _I, _D, _D, _V, _S, _I, _V], _I),
-    "mc_lab_delta_dec1p": ([_V, _V, _S, _I, _V, ctypes.c_uint, _V], _I),
-    "mc_lab_c4_dec1p": ([_V, _V, _S, _I, _I, _D, _D, _V, ctypes.c_uint, _V], _I),
+    "mc_lab_delta_dec1p_state_bytes": ([_S, _I], _S),
+    "mc_lab_c4_dec1p_state_bytes": ([_S, _I], _S),
+    "mc_lab_delta_dec1p": ([_V, _V, _S, _I, _V, ctypes.c_uint, _V, _V], _I),
+    "mc_lab_c4_dec1p": ([_V, _V, _S, _I, _I, _D, _D, _V, ctypes.c_uint, _V, _V], _I),
 }
 _lib = None
 

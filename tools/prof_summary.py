@@ -1,107 +1,127 @@
-"""Condense rocprofv3 outputs from gpurun_out/ into profiles/<round>/.
+"""Condense per-config rocprofv3 runs (tools/prof_all.sh) into
+profiles/<round>/config_profile.json.
 
-    python tools/prof_summary.py r01
+    python tools/prof_summary.py r02
 
-Reads
-  gpurun_out/prof_kt/bench_kernel_stats.csv      (--kernel-trace --stats)
-  gpurun_out/prof_kt/bench_kernel_trace.csv
-  gpurun_out/prof_fetch/bench_counter_collection.csv   (--pmc FETCH_SIZE)
-  gpurun_out/prof_write/bench_counter_collection.csv   (--pmc WRITE_SIZE)
-and writes profiles/<round>/kernel_stats.csv (names shortened) and
-profiles/<round>/pmc_summary.json.  HBM bytes per launch follow
-MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE reports exactly half of a wide streaming read, so it is doubled.
+For every CONFIG/direction directory gpurun_out/prof/<CONFIG>_<dir>_{kt,fetch,write}
+(tools/prof_configs.py under --kernel-trace, --pmc FETCH_SIZE, --pmc WRITE_SIZE):
+
+* the measured dispatches are those between the two "spin_kernel" markers
+  (by dispatch id), i.e. exactly `reps` calls of the operation;
+* kernels are keyed by their FULL name (template arguments included), never
+  by a prefix; each kernel's dispatch count must be a multiple of `reps`
+  (else the entry is marked invalid);
+* time per call = the sum of the measured kernel durations / reps; achieved
+  GB/s = the config's algorithmic bytes per call / that time (an entry above
+  the 8 TB/s peak is marked invalid);
+* HBM bytes per call = (2 * FETCH_SIZE + WRITE_SIZE) summed over the measured
+  dispatches / reps (KiB counters; gfx950 FETCH_SIZE counts half of a wide
+  streaming read -- MI355X_MICROARCH.md, HBM), and traffic_over_algorithmic.
 """
 
 import csv
+import glob
 import json
 import os
 import re
-import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "gpurun_out")
-
-KERNELS = {
-    "shuffle_enc": "k_shuffle_enc<",
-    "shuffle_dec": ("k_shuffle_dec<", "k_shuffle4_dec_pair<"),
-    "shuffle_f32_enc": "k_shuffle_f32_enc<",
-    "f32_unshuffle": "k_f32_unshuffle<",
-    "map": "k_map<",
-    "bitround": "k_bitround<",
-    "delta_enc": "k_delta_enc<",
-    "scan_reduce": "k_scan_reduce<",
-    "scan_apply": "k_scan_apply<",
-    "f32_partial": "k_f32_partial<",
-    "shuffle8_enc_pair": "k_shuffle8_enc_pair<",
-    "shuffle8_dec_pair": "k_shuffle8_dec_pair<",
-    "c4_enc": "k_c4_enc<",
-    "c4_reduce2": "k_c4_reduce2<",
-    "c4_apply": "k_c4_apply<",
-    "scan_sums": "k_scan_sums<",
-}
-ALGO_BYTES = {"shuffle_enc": 2 * 256 * 2**20, "shuffle_dec": 2 * 256 * 2**20}
-
-
-def _match(pat, name: str) -> bool:
-    return any(p in name for p in ((pat,) if isinstance(pat, str) else pat))
+OUT = os.path.join(ROOT, "gpurun_out", "prof")
+PEAK_GBPS = 8000.0
 
 
 def short(name: str) -> str:
     name = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    name = re.sub(r"\(.*$", "", name)  # drop the parameter list
-    return name[:120]
+    return re.sub(r"\(.*$", "", name)[:140]
+
+
+def _find(d, suffix):
+    f = glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True)
+    return f[0] if f else None
+
+
+def measured(rows, name_key, id_key):
+    """Rows strictly between the two spin_kernel markers (by dispatch id)."""
+    rows = sorted(rows, key=lambda r: int(r[id_key]))
+    marks = [int(r[id_key]) for r in rows if "spin_kernel" in r[name_key]]
+    if len(set(marks)) < 2:
+        return None
+    lo, hi = sorted(set(marks))[0], sorted(set(marks))[-1]
+    return [r for r in rows if lo < int(r[id_key]) < hi and "spin_kernel" not in r[name_key]]
+
+
+def one(cfg_dir_prefix, meta):
+    res = {"reps": meta["reps"], "alg_bytes_per_call": meta["alg_bytes_per_call"],
+           "event_us_per_call": meta["event_us_per_call"], "kernels": {}, "valid": True, "notes": []}
+    reps = meta["reps"]
+    kt = _find(cfg_dir_prefix + "_kt", "kernel_trace.csv")
+    if kt:
+        rows = measured(list(csv.DictReader(open(kt))), "Kernel_Name", "Dispatch_Id")
+        if rows is None:
+            res["valid"] = False
+            res["notes"].append("markers not found in the kernel trace")
+            rows = []
+        total = 0
+        for r in rows:
+            k = res["kernels"].setdefault(short(r["Kernel_Name"]), {"dispatches": 0, "total_ns": 0})
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            k["dispatches"] += 1
+            k["total_ns"] += dur
+            total += dur
+        for name, k in res["kernels"].items():
+            k["avg_ns"] = round(k["total_ns"] / k["dispatches"], 1)
+            if k["dispatches"] % reps:
+                res["valid"] = False
+                res["notes"].append(f"{name}: {k['dispatches']} dispatches for {reps} calls")
+        if rows:
+            us = total / reps / 1e3
+            res["kernel_us_per_call"] = round(us, 2)
+            res["achieved_GBps"] = round(meta["alg_bytes_per_call"] / (us * 1e3), 1)
+            res["frac_of_peak"] = round(res["achieved_GBps"] / PEAK_GBPS, 4)
+            if res["achieved_GBps"] > PEAK_GBPS:
+                res["valid"] = False
+                res["notes"].append("achieved above the 8 TB/s peak")
+    hbm = 0.0
+    have = 0
+    for sub, counter, mult in (("_fetch", "FETCH_SIZE", 2.0), ("_write", "WRITE_SIZE", 1.0)):
+        f = _find(cfg_dir_prefix + sub, "counter_collection.csv")
+        if not f:
+            continue
+        rows = list(csv.DictReader(open(f)))
+        id_key = "Dispatch_Id" if rows and "Dispatch_Id" in rows[0] else "Correlation_Id"
+        rows = measured(rows, "Kernel_Name", id_key)
+        if rows is None:
+            res["notes"].append(f"markers not found in the {counter} pass")
+            continue
+        vals = [float(r["Counter_Value"]) for r in rows if r["Counter_Name"] == counter]
+        res[counter + "_KiB_per_call"] = round(sum(vals) / reps, 1)
+        hbm += mult * sum(vals) * 1024 / reps
+        have += 1
+    if have == 2:
+        res["hbm_bytes_per_call"] = int(hbm)
+        res["traffic_over_algorithmic"] = round(hbm / meta["alg_bytes_per_call"], 4)
+    return res
 
 
 def main():
-    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    tag = sys.argv[2] if len(sys.argv) > 2 else ""  # "" = headline, "_extra" = bench.py --extra
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r02"
+    summary = {"round": rnd, "peak_GBps": PEAK_GBPS,
+               "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024) over the marked dispatches; "
+                             "MI355X_MICROARCH.md HBM section",
+               "configs": {}}
+    for meta_fn in sorted(glob.glob(os.path.join(OUT, "*_meta.json"))):
+        meta = json.load(open(meta_fn))
+        key = f"{meta['config']}_{meta['direction']}"
+        summary["configs"][key] = one(os.path.join(OUT, key), meta)
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    summary = {"round": rnd, "kernels": {}}
-    stats_fn = os.path.join(OUT, "prof_kt" + tag, "bench_kernel_stats.csv")
-    if os.path.exists(stats_fn):
-        rows = list(csv.DictReader(open(stats_fn)))
-        with open(os.path.join(dst, f"kernel_stats{tag}.csv"), "w", newline="") as f:
-            w = csv.writer(f)
-            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
-            for r in rows:
-                w.writerow([short(r["Name"]), r["Calls"], r["TotalDurationNs"], r["AverageNs"],
-                            r["Percentage"], r["MinNs"], r["MaxNs"]])
-        for key, pat in KERNELS.items():
-            for r in rows:
-                if _match(pat, r["Name"]):
-                    k = summary["kernels"].setdefault(key, {})
-                    k["name"] = short(r["Name"])
-                    k["calls"] = int(r["Calls"])
-                    k["avg_ns"] = float(r["AverageNs"])
-                    if key in ALGO_BYTES:
-                        k["algorithmic_bytes_per_launch"] = ALGO_BYTES[key]
-                        k["achieved_GBps"] = round(ALGO_BYTES[key] / float(r["AverageNs"]), 1)
-    for sub, counter in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
-        fn = os.path.join(OUT, sub + tag, "bench_counter_collection.csv")
-        if not os.path.exists(fn):
-            continue
-        rows = list(csv.DictReader(open(fn)))
-        for key, pat in KERNELS.items():
-            vals = [float(r["Counter_Value"]) for r in rows
-                    if _match(pat, r["Kernel_Name"]) and r["Counter_Name"] == counter]
-            if vals:
-                k = summary["kernels"].setdefault(key, {})
-                k[counter + "_KiB_median"] = statistics.median(vals)
-                k[counter + "_dispatches"] = len(vals)
-    for key, k in summary["kernels"].items():
-        if "FETCH_SIZE_KiB_median" in k and "WRITE_SIZE_KiB_median" in k:
-            fetch = 2 * k["FETCH_SIZE_KiB_median"] * 1024  # gfx950: FETCH_SIZE reads half
-            write = k["WRITE_SIZE_KiB_median"] * 1024
-            k["hbm_bytes_per_launch"] = int(fetch + write)
-            if key in ALGO_BYTES:
-                k["traffic_over_algorithmic"] = round((fetch + write) / ALGO_BYTES[key], 4)
-    summary["correction"] = "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024), MI355X_MICROARCH.md HBM section"
-    with open(os.path.join(dst, f"pmc_summary{tag}.json"), "w") as f:
+    with open(os.path.join(dst, "config_profile.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    print(json.dumps(summary, indent=1))
+    for k, v in summary["configs"].items():
+        print(f"{k:12s} {v.get('kernel_us_per_call', '-'):>9} us  {v.get('achieved_GBps', '-'):>8} GB/s  "
+              f"frac {v.get('frac_of_peak', '-'):>7}  traffic/alg {v.get('traffic_over_algorithmic', '-'):>7}  "
+              f"valid {v['valid']} {'; '.join(v['notes'])}")
 
 
 if __name__ == "__main__":
