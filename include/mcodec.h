@@ -51,12 +51,17 @@ extern "C" {
 
 typedef void *mc_stream_t; /* hipStream_t */
 
-#define MC_ABI_VERSION 1
+#define MC_ABI_VERSION 2
 
 /* status codes */
 #define MC_OK 0
 #define MC_EINVAL (-22)      /* bad argument (size, dtype, alignment, NULL) */
 #define MC_ENOSPC (-28)      /* workspace too small */
+#define MC_EPROTO (-71)      /* a stream ended without publishing its verdict */
+
+/* Size in uint32 words of the arrival counter (`ticket`) that the one-launch
+ * verifies take: 64 shard words on separate 128-B lines plus a top word. */
+#define MC_ARRIVAL_WORDS 2080
 #define MC_EHIP_BASE (-1000) /* MC_EHIP_BASE - (int)hipError_t */
 
 /* dtype codes (little-endian numpy dtypes; numpy kind + itemsize) */
@@ -198,15 +203,16 @@ int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes,
 int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair,
                          void *workspace, size_t workspace_bytes,
                          mc_stream_t stream);
-/* mc_fletcher32_verify in ONE launch: the checksum's last block folds the
- * partials (no finalize kernel).  `ticket`: 16 device uint32 words (an
- * arrival counter), zero before the first call and left zero by every call
- * (keep one per stream);
- * NULL = mc_fletcher32_verify.  out_pair may be host-mapped pinned memory
- * (hipHostMalloc): the caller then reads the verdict after one stream sync,
- * with no device-to-host copy. */
-int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_pair,
-                               void *workspace, size_t workspace_bytes,
+/* mc_fletcher32_verify in ONE launch: the checksum's last blocks fold the
+ * partials (no finalize kernel).  `ticket`: MC_ARRIVAL_WORDS device uint32
+ * words (an arrival counter), zero before the first call and left zero by every call
+ * (keep one per stream); NULL = mc_fletcher32_verify (seq must be 0).
+ * out_rec = {computed, stored, seq, -}: with seq != 0 the kernel writes
+ * out_rec[2] = seq after the verdict, so with out_rec = the device address of
+ * an mc_verdict_alloc record the caller waits with mc_verdict_wait (no stream
+ * synchronisation, no device-to-host copy); seq == 0 writes words 0-1 only. */
+int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_rec,
+                               uint32_t seq, void *workspace, size_t workspace_bytes,
                                uint32_t *ticket, mc_stream_t stream);
 /* out_sums[c] = fletcher32(chunk c), chunk c = src + c*stride, chunk_bytes. */
 size_t mc_fletcher32_batch_workspace(size_t nchunks, size_t chunk_bytes);
@@ -329,12 +335,13 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride,
 /* Checksum32.decode's verification of ONE encoded buffer (payload + 4 bytes
  * at `location`) in one launch: out_pair[0] = checksum of the payload,
  * out_pair[1] = the stored LE32 value (the caller compares and raises).
- * `ticket` and out_pair as for mc_fletcher32_verify_fused; workspace:
- * mc_checksum32_workspace(kind, 1, encoded_bytes - 4). */
+ * `ticket`, out_pair and seq as for mc_fletcher32_verify_fused (seq != 0
+ * needs a ticket and is refused for Jenkins, which has no one-launch fold);
+ * workspace: mc_checksum32_workspace(kind, 1, encoded_bytes - 4). */
 int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes,
                                uint32_t init, const void *prefix,
                                size_t prefix_bytes, int location,
-                               uint32_t *out_pair, void *workspace,
+                               uint32_t *out_pair, uint32_t seq, void *workspace,
                                size_t workspace_bytes, uint32_t *ticket,
                                mc_stream_t stream);
 
@@ -345,6 +352,17 @@ int mc_stream_synchronize(mc_stream_t stream);
  * NULL if `host` is not mapped: where a kernel may write a host-visible
  * verdict. */
 void *mc_host_device_pointer(void *host);
+/* A 64-B verdict record {computed, stored, seq, ...} in fine-grained mapped
+ * pinned host memory (hipHostMalloc Mapped|Coherent|Portable), seq word 0;
+ * NULL on failure.  Pass mc_host_device_pointer(rec) as a fused verify's
+ * out_rec/out_pair. */
+void *mc_verdict_alloc(void);
+void mc_verdict_free(void *rec);
+/* Spin until rec[2] == seq (seq != 0), polling hipStreamQuery(stream) every
+ * ~1K spins: MC_OK when the record is published; MC_EPROTO if the stream
+ * ended without publishing it; the stream's HIP error if it failed.  Replaces
+ * the stream synchronisation of a verified decode (~6 us less latency). */
+int mc_verdict_wait(const uint32_t *rec, uint32_t seq, mc_stream_t stream);
 
 /* ---- PackBits (packbits.py:33-82) --------------------------------------- */
 /* encode n bools (any nonzero byte is True) into dst[0] = padding bits

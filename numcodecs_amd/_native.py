@@ -49,6 +49,8 @@ DTYPE_CODES = {
 MC_OK = 0
 MC_EINVAL = -22
 MC_ENOSPC = -28
+MC_EPROTO = -71
+MC_ARRIVAL_WORDS = 2080  # include/mcodec.h: 64 shard lines + a top line
 MC_EHIP_BASE = -1000
 
 
@@ -99,7 +101,7 @@ _SIGNATURES = {
     "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_verify": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
-    "mc_fletcher32_verify_fused": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp, _c_vp],
+    "mc_fletcher32_verify_fused": [_c_vp, _c_size, _c_vp, _c_u32, _c_vp, _c_size, _c_vp, _c_vp],
     "mc_fletcher32_batch_workspace": [_c_size, _c_size],
     "mc_fletcher32_batch": [_c_vp, _c_size, _c_size, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp, _c_size, _c_vp],
@@ -129,10 +131,13 @@ _SIGNATURES = {
         _c_vp, _c_vp, _c_vp, _c_size, _c_vp,
     ],
     "mc_checksum32_verify_fused": [
-        _c_int, _c_vp, _c_size, _c_u32, _c_vp, _c_size, _c_int, _c_vp, _c_vp, _c_size, _c_vp, _c_vp,
+        _c_int, _c_vp, _c_size, _c_u32, _c_vp, _c_size, _c_int, _c_vp, _c_u32, _c_vp, _c_size, _c_vp, _c_vp,
     ],
     "mc_stream_synchronize": [_c_vp],
     "mc_host_device_pointer": [_c_vp],
+    "mc_verdict_alloc": [],
+    "mc_verdict_free": [_c_vp],
+    "mc_verdict_wait": [_c_vp, _c_u32, _c_vp],
     "mc_packbits": [_c_vp, _c_vp, _c_size, _c_vp],
     "mc_copy": [_c_vp, _c_vp, _c_size, _c_vp],
     "mc_copy_rows": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_vp],
@@ -141,6 +146,8 @@ _SIGNATURES = {
 }
 _RESTYPES = {
     "mc_host_device_pointer": ctypes.c_void_p,
+    "mc_verdict_alloc": ctypes.c_void_p,
+    "mc_verdict_free": None,
     "mc_strerror": ctypes.c_char_p,
     "mc_delta_decode_workspace": ctypes.c_size_t,
     "mc_delta_decode_batch_workspace": ctypes.c_size_t,

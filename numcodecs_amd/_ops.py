@@ -9,12 +9,13 @@ synchronises except where a result must be inspected on the host
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import numpy as np
 import torch
 
 from . import _native
-from ._native import DTYPE_CODES, check, lib
+from ._native import DTYPE_CODES, MC_ARRIVAL_WORDS, check, lib
 
 __all__ = ["dtype_code", "stream", "workspace"]
 
@@ -49,26 +50,48 @@ def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
 class _VerifySlot:
     """Per-(device, stream) resources of the one-launch checksum verify: a
     zeroed arrival counter (left zero by every call), a reusable partials
-    workspace and a pinned host pair the kernel writes its verdict into."""
+    workspace and a verdict record in mapped, fine-grained pinned host memory
+    (mc_verdict_alloc) that the kernel writes {computed, stored, seq} into;
+    the host spins on the seq word (mc_verdict_wait) instead of synchronising
+    the stream."""
 
     def __init__(self, device):
         self.device = device
-        self.ticket = torch.zeros(16, dtype=torch.int32, device=device)  # MC_ARRIVAL_WORDS
+        self.ticket = torch.zeros(MC_ARRIVAL_WORDS, dtype=torch.int32, device=device)
         self.ws = torch.empty(1 << 20, dtype=torch.uint8, device=device)
-        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-        self.host_np = self.host.numpy().view(np.uint32)
-        # the kernel writes the verdict through the pinned buffer's device
-        # address; if it is not mapped, into device memory + one async copy
-        self.out_ptr = lib.mc_host_device_pointer(self.host.data_ptr())
-        self.dev = None if self.out_ptr else torch.zeros(2, dtype=torch.int32, device=device)
-        if self.dev is not None:
-            self.out_ptr = self.dev.data_ptr()
+        self.rec = lib.mc_verdict_alloc()
+        if not self.rec:
+            raise _native.MCodecError("mc_verdict_alloc failed (mapped pinned host memory)")
+        self.rec_np = np.ctypeslib.as_array((ctypes.c_uint32 * 4).from_address(self.rec))
+        self.out_ptr = lib.mc_host_device_pointer(self.rec)
+        if not self.out_ptr:
+            raise _native.MCodecError("the verdict record is not mapped into the device address space")
+        self.seq = 0
+        self.ws_sizes = {}
 
-    def read(self, st):
-        if self.dev is not None:
-            self.host.copy_(self.dev, non_blocking=True)
-        check(lib.mc_stream_synchronize(st), "mc_stream_synchronize")
-        return int(self.host_np[0]), int(self.host_np[1])
+    def next_seq(self) -> int:
+        """The sequence word of the next verify (1 .. 2**32 - 1, never 0)."""
+        self.seq = self.seq % 0xFFFFFFFF + 1
+        return self.seq
+
+    def read(self, st, seq):
+        """(computed, stored) once the kernel published `seq` (0: after a
+        stream synchronisation, for kernels that publish no sequence word)."""
+        if seq:
+            check(lib.mc_verdict_wait(self.rec, seq, st), "mc_verdict_wait")
+        else:
+            check(lib.mc_stream_synchronize(st), "mc_stream_synchronize")
+        return int(self.rec_np[0]), int(self.rec_np[1])
+
+    def workspace_for(self, key, query):
+        """The workspace for a verify of `key` = (entry point, sizes...): the
+        size query runs once per key."""
+        n = self.ws_sizes.get(key)
+        if n is None:
+            if len(self.ws_sizes) >= 256:  # bounded: many distinct chunk sizes
+                self.ws_sizes.clear()
+            n = self.ws_sizes[key] = int(query())
+        return self.workspace(n)
 
     def workspace(self, nbytes):
         if self.ws.numel() < nbytes:
@@ -259,10 +282,11 @@ def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
         st = stream(src)
         sl = _verify_slot(src, st)
         if sl is not None:
-            ws = sl.workspace(lib.mc_fletcher32_workspace(nbytes))
-            check(lib.mc_fletcher32_verify_fused(src.data_ptr(), nbytes, sl.out_ptr, ws.data_ptr(),
+            ws = sl.workspace_for(("f32", nbytes), lambda: lib.mc_fletcher32_workspace(nbytes))
+            seq = sl.next_seq()
+            check(lib.mc_fletcher32_verify_fused(src.data_ptr(), nbytes, sl.out_ptr, seq, ws.data_ptr(),
                                                  ws.numel(), sl.ticket.data_ptr(), st), "mc_fletcher32_verify_fused")
-            return sl.read(st)
+            return sl.read(st, seq)
         ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
         pair = torch.empty(2, dtype=torch.int32, device=src.device)
         check(lib.mc_fletcher32_verify(src.data_ptr(), nbytes, pair.data_ptr(), ws.data_ptr(),
@@ -360,14 +384,16 @@ def checksum32_verify(kind, src, encoded_bytes, init, location, prefix=None) -> 
         pre = _prefix_dev(prefix, src)
         st = stream(src)
         sl = _verify_slot(src, st)
-        if sl is not None:  # one launch, verdict into pinned host memory, one sync
-            ws = sl.workspace(lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4))
+        if sl is not None:  # one launch, verdict into pinned host memory, one host wait
+            ws = sl.workspace_for((kind, encoded_bytes),
+                                  lambda: lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4))
+            seq = 0 if kind == _native.MC_CK_JENKINS else sl.next_seq()
             check(lib.mc_checksum32_verify_fused(kind, src.data_ptr(), encoded_bytes, init & 0xFFFFFFFF,
                                                  pre.data_ptr() if pre is not None else None,
                                                  pre.numel() if pre is not None else 0, location,
-                                                 sl.out_ptr, ws.data_ptr(), ws.numel(),
+                                                 sl.out_ptr, seq, ws.data_ptr(), ws.numel(),
                                                  sl.ticket.data_ptr(), st), "mc_checksum32_verify_fused")
-            return sl.read(st)
+            return sl.read(st, seq)
         pair = torch.empty(2, dtype=torch.int32, device=src.device)
         ws = workspace(lib.mc_checksum32_workspace(kind, 1, encoded_bytes - 4), src)
         check(lib.mc_checksum32_decode_batch(kind, src.data_ptr(), encoded_bytes, None, 0, 1, encoded_bytes,

@@ -175,6 +175,9 @@ def download(dev: torch.Tensor) -> np.ndarray:
     return host.numpy()
 
 
+_U8 = np.dtype(np.uint8)
+
+
 @dataclass
 class DBuf:
     """Raw bytes on the device + the numpy array they stand for."""
@@ -211,6 +214,10 @@ def to_dbuf(buf, *, flatten=True, contiguous=True) -> DBuf:
     C order, as the reference's ``reshape(-1, order='A')`` would) and are
     uploaded; device tensors are used in place.
     """
+    if (type(buf) is torch.Tensor and buf.dtype is torch.uint8 and buf.dim() == 1 and buf.is_cuda
+            and buf.is_contiguous()):
+        # the common case (an encoded chunk): flat device bytes, used as they are
+        return DBuf(buf, _U8, (buf.numel(),), "C", False)
     if is_device_tensor(buf):
         order = _tensor_order(buf)
         if order is None:

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_finalize(
 // folds them in the same launch (ck_finish_chunk) and zeroes the counter
 // again -- one launch, no finalize boundary.
 struct CkFinish {
-  uint32_t init;
+  uint32_t init, seq;  // seq: published after the verdict (mc_publish_verdict_seq)
   uint32_t *ticket, *out, *stored_out;
   uint8_t *footer;
   size_t footer_stride;
@@ -430,7 +430,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
     if (!last) return;
     ck_finish_chunk<KIND, K, true>(fin, partials, tiles_per_chunk, n, fx.init, fx.out, fx.footer,
                                    fx.footer_stride, fx.stored, src_stride, fx.stored_out, 0);
-    if (threadIdx.x == 0) mc_arrivals_reset(fx.ticket);  // left zero for the next launch
+    if (threadIdx.x == 0) {  // thread 0 wrote both verdict words
+      mc_publish_verdict_seq(fx.out, fx.seq);
+      mc_arrivals_reset(fx.ticket);  // left zero for the next launch
+    }
   }
 }
 
@@ -717,7 +720,8 @@ const CrcFin &crc_fin(int K, size_t tpc, size_t n) {
 template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
                   uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
-                  uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st, uint32_t *ticket) {
+                  uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st, uint32_t *ticket,
+                  uint32_t seq) {
   const int K = ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
@@ -726,7 +730,7 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   // one chunk, no copy, with a ticket: finish in the tiles launch
   // (ck_finish_chunk)
   const bool fused = ticket && nchunks == 1 && !d;
-  const CkFinish fx{init, ticket, out, stored_out, footer, fs, stored};
+  const CkFinish fx{init, seq, ticket, out, stored_out, footer, fs, stored};
   switch (K) {
 #define MC_CK_CASE(KK)                                                                         \
   case KK: {                                                                                   \
@@ -751,17 +755,17 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
 int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks,
                 size_t n, uint32_t init, const uint8_t *prefix, size_t plen, uint32_t *out,
                 uint8_t *footer, size_t fs, const uint8_t *stored, uint32_t *stored_out, void *ws,
-                size_t ws_bytes, hipStream_t st, uint32_t *ticket = nullptr) {
+                size_t ws_bytes, hipStream_t st, uint32_t *ticket = nullptr, uint32_t seq = 0) {
   switch (kind) {
     case MC_CK_CRC32:
       return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st, ticket);
+                                    ws, ws_bytes, st, ticket, seq);
     case MC_CK_CRC32C:
       return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                     ws, ws_bytes, st, ticket);
+                                     ws, ws_bytes, st, ticket, seq);
     case MC_CK_ADLER32:
       return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st, ticket);
+                                    ws, ws_bytes, st, ticket, seq);
     case MC_CK_JENKINS: {
       if (d && n) {
         const int rc = mc_copy_rows_impl(s, ss, d, ds, n, nchunks, st);
@@ -852,10 +856,12 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride, voi
 // (keep one per stream); NULL = the two-launch path.
 int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, uint32_t init,
                                const void *prefix, size_t prefix_bytes, int location, uint32_t *out_pair,
-                               void *workspace, size_t workspace_bytes, uint32_t *ticket,
+                               uint32_t seq, void *workspace, size_t workspace_bytes, uint32_t *ticket,
                                mc_stream_t stream) {
   if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
   if (encoded_bytes < 4 || !src || !out_pair) return MC_EINVAL;
+  // only the one-launch finish of CRC32 / CRC32C / Adler32 publishes `seq`
+  if (seq && (!ticket || kind == MC_CK_JENKINS)) return MC_EINVAL;
   if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
   const size_t n = encoded_bytes - 4;
   const uint8_t *s = static_cast<const uint8_t *>(src);
@@ -863,7 +869,7 @@ int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, 
   const uint8_t *stored = location == MC_CK_START ? s : s + n;
   return ck_dispatch(kind, payload, encoded_bytes, nullptr, 0, 1, n, init, static_cast<const uint8_t *>(prefix),
                      prefix_bytes, out_pair, nullptr, 0, stored, out_pair + 1, workspace, workspace_bytes,
-                     (hipStream_t)stream, ticket);
+                     (hipStream_t)stream, ticket, seq);
 }
 
 }  // extern "C"

@@ -76,29 +76,55 @@ static constexpr int MC_BLOCK = 256;  // 4 waves of 64 lanes
 
 // ---------------------------------------------------------------------------
 // "Last block arrives" for an in-launch finish (no finalize kernel): an
-// arrival counter sharded 8 ways (tickets[0..7], block b counts in shard
-// b % 8, as blocks are dealt round-robin over the 8 XCDs) plus
-// tickets[8] = shards completed.  One word alone saturates at ~88 atomics/us
-// (MI355X_MICROARCH.md, "dequeue"/"fanin"): 8192 arrivals on it took ~90 us.
-// Called by thread 0 of every block, after the block's hand-off stores and an
-// `s_waitcnt vmcnt(0)`; true in exactly one block -- the last -- which then
-// finishes and calls mc_arrivals_reset (every other arrival is done by then,
-// so the words are left zero for the next launch).  MC_ARRIVAL_WORDS words,
-// zero before the first launch.
+// arrival counter sharded MC_ARRIVAL_SHARDS ways, block b counting in shard
+// b % 64, each shard word on its own 128-B line (word 32*s), plus a top word
+// (word 32*64) counting completed shards.  Device-scope atomics on one line
+// serialise at ~88 per us (MI355X_MICROARCH.md, "dequeue"/"fanin"): 8192
+// arrivals on 8 words of ONE line took the whole 256 MiB verify from 50 to
+// 110 us; 64 lines take ~128 arrivals each.  Called by thread 0 of every
+// block after the block's hand-off stores and an `s_waitcnt vmcnt(0)`:
+// mc_arrive_shard is true in the last block of a shard, mc_arrive_top (called
+// by exactly those) true in the last of them, which finishes and calls
+// mc_arrivals_reset (every other arrival is done by then, so the words are
+// left zero for the next launch).  MC_ARRIVAL_WORDS (include/mcodec.h)
+// words, zero before the first launch.
 // ---------------------------------------------------------------------------
-static constexpr int MC_ARRIVAL_WORDS = 16;
+static constexpr unsigned MC_ARRIVAL_SHARDS = 64;
+static constexpr unsigned MC_ARRIVAL_LINE = 32;  // words per 128-B line
+static_assert(MC_ARRIVAL_WORDS == (MC_ARRIVAL_SHARDS + 1) * MC_ARRIVAL_LINE, "arrival counter layout");
 
+__device__ inline unsigned mc_arrival_shard(unsigned b) { return b % MC_ARRIVAL_SHARDS; }
+// blocks b < nblocks in shard s
+__device__ inline unsigned mc_arrival_per(unsigned s, unsigned nblocks) {
+  return nblocks > s ? (nblocks - s + MC_ARRIVAL_SHARDS - 1) / MC_ARRIVAL_SHARDS : 0u;
+}
+__device__ inline unsigned mc_arrival_nshards(unsigned nblocks) {
+  return nblocks < MC_ARRIVAL_SHARDS ? nblocks : MC_ARRIVAL_SHARDS;
+}
+__device__ inline bool mc_arrive_shard(uint32_t *tickets, unsigned nblocks) {
+  const unsigned s = mc_arrival_shard(blockIdx.x);
+  return atomicAdd(&tickets[MC_ARRIVAL_LINE * s], 1u) == mc_arrival_per(s, nblocks) - 1u;
+}
+__device__ inline bool mc_arrive_top(uint32_t *tickets, unsigned nblocks) {
+  return atomicAdd(&tickets[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS], 1u) == mc_arrival_nshards(nblocks) - 1u;
+}
 __device__ inline bool mc_arrive_last(uint32_t *tickets, unsigned nblocks) {
-  const unsigned s = blockIdx.x & 7u;
-  const unsigned nshards = nblocks < 8u ? nblocks : 8u;
-  const unsigned per = (nblocks - s + 7u) / 8u;  // blocks b < nblocks with b % 8 == s
-  if (atomicAdd(&tickets[s], 1u) != per - 1u) return false;
-  return atomicAdd(&tickets[8], 1u) == nshards - 1u;
+  return mc_arrive_shard(tickets, nblocks) && mc_arrive_top(tickets, nblocks);
 }
 
 __device__ inline void mc_arrivals_reset(uint32_t *tickets) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) tickets[i] = 0;
+  for (unsigned i = 0; i <= MC_ARRIVAL_SHARDS; ++i) tickets[MC_ARRIVAL_LINE * i] = 0;
+}
+
+// A single-chunk verify's verdict record {computed, stored, seq, -} (host-
+// mapped pinned memory, mc_verdict_alloc): after writing words 0-1 the
+// finishing thread publishes `seq` in word 2 behind a system-scope release,
+// so a host polling word 2 (mc_verdict_wait) reads a complete verdict without
+// a stream synchronisation.  seq == 0: nothing is published.
+__device__ inline void mc_publish_verdict_seq(uint32_t *rec, uint32_t seq) {
+  if (!seq) return;
+  __threadfence_system();
+  __hip_atomic_store(rec + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // grid cap for grid-stride streaming kernels: 256 CUs x 8 blocks of 256 threads

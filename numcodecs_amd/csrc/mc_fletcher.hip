@@ -159,18 +159,18 @@ MC_DEV uint32_t part_ld(const uint32_t *p) {
 template <bool SC1>
 MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t c, int mode,
                              const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
-                             size_t nbytes, uint32_t *out);
+                             size_t nbytes, uint32_t *out, uint32_t seq = 0);
 
 // block = (chunk c, slice sl), partials[block] = {S1, S2, nz}; or, with
-// `tickets` (one chunk, FUSED finish): a persistent grid, block b sums slices
-// b, b + grid, ... (absolute weights: slice partials add), stores ONE partial
-// sc1, arrives (mc_arrive_last) and the last block folds the grid's partials
-// and finishes the chunk in this launch
+// `tickets` (one chunk, FUSED finish): block b sums slices b, b + grid, ...
+// (absolute weights: slice partials add; the launch gives one slice per
+// block), stores ONE partial sc1 and arrives; the fold runs in this launch
+// (below).  `seq` != 0: F_VERIFY publishes out[2] = seq after the verdict
 template <bool COPY, int AL, int F32_UNROLL, bool NT>
 __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
     size_t dst_stride, size_t nbytes, unsigned nslices, uint32_t *__restrict__ partials,
-    uint32_t *tickets, int mode, uint32_t *out) {
+    uint32_t *tickets, int mode, uint32_t *out, uint32_t seq) {
   const size_t c = tickets ? 0 : blockIdx.x / nslices;
   const unsigned sl0 = tickets ? blockIdx.x : blockIdx.x - (unsigned)(c * nslices);
   const unsigned sl_step = tickets ? gridDim.x : nslices;
@@ -227,27 +227,55 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     }
     return;
   }
-  // fused finish: the last block to arrive folds the grid's partials in this
-  // launch (no finalize kernel, no extra boundary)
+  // fused finish in two levels, in this launch (no finalize kernel, no extra
+  // boundary): block b arrives in shard sh = b % 64 (mc_arrive_shard); the
+  // last block of a shard folds that shard's partials (shard-major:
+  // partials[sh * per_max + b / 64]) while other shards still stream, and the
+  // last of the shard folders (mc_arrive_top) finishes the chunk from the
+  // shard sums (partials[64 * per_max + sh]).
   __shared__ uint32_t last;
+  const unsigned sh = mc_arrival_shard(blockIdx.x);
+  const unsigned per_max = (gridDim.x + MC_ARRIVAL_SHARDS - 1) / MC_ARRIVAL_SHARDS;
+  const unsigned per = mc_arrival_per(sh, gridDim.x);
   if (threadIdx.x == 0) {
-    uint32_t *q = partials + 3 * (size_t)blockIdx.x;
+    uint32_t *q = partials + 3 * ((size_t)sh * per_max + blockIdx.x / MC_ARRIVAL_SHARDS);
     __hip_atomic_store(q + 0, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(q + 1, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(q + 2, nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = mc_arrive_last(tickets, gridDim.x);
+    last = mc_arrive_shard(tickets, gridDim.x);
   }
   __syncthreads();
   if (!last) return;
-  f32_finish_chunk<true>(partials, gridDim.x, 0, mode, src, src_stride, dst, dst_stride, nbytes, out);
+  F32Part f;
+  part_init(f);
+  for (unsigned i = threadIdx.x; i < per; i += MC_BLOCK) {
+    const uint32_t *q = partials + 3 * ((size_t)sh * per_max + i);
+    f.s1 += part_ld<true>(q);
+    f.s2a += part_ld<true>(q + 1);  // partial S2 already reduced: s2b stays 0
+    f.nz |= part_ld<true>(q + 2);
+  }
+  block_reduce(f, s1, s2, nz);
+  uint32_t *shard_sums = partials + 3 * (size_t)MC_ARRIVAL_SHARDS * per_max;
+  if (threadIdx.x == 0) {
+    uint32_t *q = shard_sums + 3 * sh;
+    __hip_atomic_store(q + 0, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = mc_arrive_top(tickets, gridDim.x);
+  }
+  __syncthreads();
+  if (!last) return;
+  f32_finish_chunk<true>(shard_sums, mc_arrival_nshards(gridDim.x), 0, mode, src, src_stride, dst, dst_stride,
+                         nbytes, out, seq);
   if (threadIdx.x == 0) mc_arrivals_reset(tickets);
 }
 
 template <bool SC1>
 MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t c, int mode,
                              const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
-                             size_t nbytes, uint32_t *out) {
+                             size_t nbytes, uint32_t *out, uint32_t seq) {
   F32Part p;
   part_init(p);
 #pragma unroll 8
@@ -269,6 +297,7 @@ MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t 
   } else {
     out[2 * c] = f;
     out[2 * c + 1] = load_le32(src + c * src_stride + nbytes);
+    mc_publish_verdict_seq(out, seq);
   }
 }
 
@@ -391,6 +420,12 @@ static unsigned slices_for(size_t nbytes, size_t nchunks) {
 static size_t partials_bytes(size_t nchunks, unsigned nslices) {
   return nchunks * (size_t)nslices * 3 * sizeof(uint32_t);
 }
+// the fused verify's shard-major partials (64 shards of ceil(nslices / 64))
+// plus the 64 shard sums
+static size_t fused_partials_bytes(unsigned nslices) {
+  const size_t per_max = ((size_t)nslices + MC_ARRIVAL_SHARDS - 1) / MC_ARRIVAL_SHARDS;
+  return (per_max + 1) * MC_ARRIVAL_SHARDS * 3 * sizeof(uint32_t);
+}
 
 // knobs (read once): MCODEC_F32_UNROLL = vectors in flight per thread in
 // k_f32_partial (1, 4, 8); MCODEC_F32_NTLD = nontemporal loads (0/1);
@@ -412,6 +447,14 @@ static bool f32_ntld() {
   static const bool b = f32_env("MCODEC_F32_NTLD", 1) != 0;
   return b;
 }
+// MCODEC_F32_FUSED_GRID: block cap of the one-launch verify (256 .. 65536)
+static unsigned f32_fused_grid() {
+  static const unsigned g = [] {
+    const int e = f32_env("MCODEC_F32_FUSED_GRID", 2048);
+    return (unsigned)(e >= 256 && e <= 65536 ? e : 2048);
+  }();
+  return g;
+}
 static size_t f32_slice_bytes() {
   static const size_t b = [] {
     const int e = f32_env("MCODEC_F32_SLICE_KB", 32);
@@ -427,25 +470,27 @@ static int align_class(const void *p, size_t stride, size_t nchunks) {
 
 static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                            size_t nchunks, size_t nbytes, unsigned nsl, uint32_t *partials,
-                           uint32_t *tickets, int mode, uint32_t *out, hipStream_t st) {
+                           uint32_t *tickets, int mode, uint32_t *out, uint32_t seq, hipStream_t st) {
   int al = align_class(src, src_stride, nchunks);
   if (dst) {
     const int ad = align_class(dst, dst_stride, nchunks);
     al = al < ad ? al : ad;
   }
-  // fused (one chunk): a persistent grid of at most 1024 blocks, so that the
-  // last block folds at most 1024 partials
-  const unsigned grid = tickets ? (nsl < 1024u ? nsl : 1024u) : (unsigned)(nchunks * nsl);
+  // fused (one chunk): at most f32_fused_grid() blocks, each summing
+  // nsl / grid slices (loads only, so a looping block keeps its loads in
+  // flight); the two-level fold (64 shards) keeps the tail short
+  const unsigned fg = f32_fused_grid();
+  const unsigned grid = tickets ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
 #define MC_F32_U(CP, AL, U)                                                                   \
   do {                                                                                         \
     if (f32_ntld())                                                                            \
       k_f32_partial<CP, AL, U, true><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,          \
                                                                 dst_stride, nbytes, nsl,       \
-                                                                partials, tickets, mode, out); \
+                                                                partials, tickets, mode, out, seq); \
     else                                                                                       \
       k_f32_partial<CP, AL, U, false><<<grid, MC_BLOCK, 0, st>>>(src, src_stride, dst,         \
                                                                  dst_stride, nbytes, nsl,      \
-                                                                 partials, tickets, mode, out);\
+                                                                 partials, tickets, mode, out, seq);\
   } while (0)
 #define MC_F32_LAUNCH(CP, AL)                                                                 \
   do {                                                                                         \
@@ -471,15 +516,16 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
 // words, left zeroed; one chunk only) is given, else as a second launch
 static int f32_run(const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                    size_t nchunks, size_t nbytes, int mode, uint32_t *out, void *ws,
-                   size_t ws_bytes, hipStream_t st, uint32_t *tickets = nullptr) {
+                   size_t ws_bytes, hipStream_t st, uint32_t *tickets = nullptr, uint32_t seq = 0) {
   const unsigned nsl = slices_for(nbytes, nchunks);
-  if (!ws || ws_bytes < partials_bytes(nchunks, nsl)) return MC_ENOSPC;
+  const size_t need = tickets ? fused_partials_bytes(nsl) : partials_bytes(nchunks, nsl);
+  if (!ws || ws_bytes < need) return MC_ENOSPC;
   uint32_t *partials = static_cast<uint32_t *>(ws);
   // F_FOOTER copies the payload in front of its footer; F_VERIFY with a dst
   // compacts the payloads out of the encoded rows (the decode pass)
   const bool copy = dst != nullptr;
   launch_partial(src, src_stride, copy ? dst : nullptr, dst_stride, nchunks, nbytes, nsl, partials, tickets, mode,
-                 out, st);
+                 out, seq, st);
   int rc = mc_last_launch();
   if (rc != MC_OK || tickets) return rc;
   k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(partials, nsl, nchunks, mode, src, src_stride,
@@ -510,7 +556,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
 extern "C" {
 
 size_t mc_fletcher32_workspace(size_t nbytes) {
-  return partials_bytes(1, slices_for(nbytes, 1));
+  return fused_partials_bytes(slices_for(nbytes, 1));  // >= partials_bytes(1, .)
 }
 
 int mc_fletcher32(const void *src, size_t nbytes, uint32_t *out_sum, void *workspace,
@@ -538,13 +584,16 @@ int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair, voi
                  workspace, workspace_bytes, st);
 }
 
-int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_pair, void *workspace,
+int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_rec, uint32_t seq, void *workspace,
                                size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
-  if (!ticket) return mc_fletcher32_verify(src, nbytes, out_pair, workspace, workspace_bytes, stream);
+  if (!ticket) {
+    if (seq) return MC_EINVAL;  // the two-launch path publishes no sequence word
+    return mc_fletcher32_verify(src, nbytes, out_rec, workspace, workspace_bytes, stream);
+  }
   if ((uintptr_t)ticket % 4) return MC_EINVAL;
-  if (!src || !out_pair || nbytes < 4) return MC_EINVAL;
-  return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, nbytes - 4, F_VERIFY, out_pair, workspace,
-                 workspace_bytes, (hipStream_t)stream, ticket);
+  if (!src || !out_rec || nbytes < 4) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, nbytes - 4, F_VERIFY, out_rec, workspace,
+                 workspace_bytes, (hipStream_t)stream, ticket, seq);
 }
 
 int mc_fletcher32_batch(const void *src, size_t stride, size_t nchunks, size_t chunk_bytes,
@@ -619,7 +668,7 @@ int mc_shuffle_fletcher32_encode_batch(const void *src, size_t src_stride, void 
     if (rc != MC_OK) return rc;
     const unsigned nsl = slices_for(chunk_bytes, nchunks);
     uint32_t *partials = static_cast<uint32_t *>(workspace);
-    launch_partial(d, dst_stride, nullptr, 0, nchunks, chunk_bytes, nsl, partials, nullptr, F_SUM, nullptr, st);
+    launch_partial(d, dst_stride, nullptr, 0, nchunks, chunk_bytes, nsl, partials, nullptr, F_SUM, nullptr, 0, st);
     rc = mc_last_launch();
     if (rc != MC_OK) return rc;
     k_f32_finalize<<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(
