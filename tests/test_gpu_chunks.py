@@ -1,16 +1,19 @@
-"""Zarr-style chunk pipelines (numcodecs_amd.chunks):
-batched encode/decode of [B, chunk] device batches and host-streamed batches
-must give, row by row, the bytes of the codecs applied one after another to
-that chunk (which the other suites pin to the reference)."""
+"""Zarr-style chunk pipelines (numcodecs_amd.chunks / batch, SURVEY.md §8f
+row 1) pinned to the ORACLE row by row: every row of a batched, host-streamed
+or padded-stride batch must equal the oracle's codecs applied one after
+another to that chunk (tests/oracle_chain.py; the reference harness shape is
+tests/common.py:51-116 of numcodecs), encode and decode."""
 
 import numpy as np
 import pytest
 import torch
 
+import oracle
 from numcodecs_amd import (
     CRC32, CRC32C, Adler32, AsType, BitRound, Delta, FixedScaleOffset, Fletcher32, JenkinsLookup3,
-    PackBits, Quantize, Shuffle, chunks,
+    PackBits, Quantize, Shuffle, batch, chunks,
 )
+from tests import oracle_chain
 
 pytestmark = pytest.mark.gpu
 
@@ -23,6 +26,9 @@ def _chains():
         "quantize_shuffle_fletcher32": ([Quantize(3, "<f8", "<f4"), Shuffle(4), Fletcher32()], torch.float64),
         "astype_shuffle_jenkins": ([AsType("<f4", "<f8"), Shuffle(4), JenkinsLookup3(initval=7)], torch.float64),
         "delta_shuffle_crc32c": ([Delta(dtype="<i4"), Shuffle(4), CRC32C()], torch.int32),
+        "bitround_shuffle_fletcher32": ([BitRound(12), Shuffle(4), Fletcher32()], torch.float32),
+        "delta_i8_i2_shuffle_crc32": ([Delta(dtype="<i8", astype="<i2"), Shuffle(2), CRC32(location="end")],
+                                      torch.int64),
         "packbits": ([PackBits()], torch.bool),
     }
 
@@ -31,36 +37,35 @@ def _make(dtype, b, n, device, seed):
     g = torch.Generator(device=device).manual_seed(seed)
     if dtype == torch.bool:
         return torch.randint(0, 2, (b, n), generator=g, device=device).to(torch.bool)
-    if dtype == torch.int32:
-        return torch.randint(-1000, 1000, (b, n), generator=g, device=device, dtype=torch.int32)
+    if dtype in (torch.int32, torch.int64):
+        return torch.randint(-1000, 1000, (b, n), generator=g, device=device, dtype=dtype)
     return (1000 + 10 * torch.rand((b, n), generator=g, device=device)).to(dtype)
 
 
-def _seq_encode(codecs, x):
-    for c in codecs:
-        x = c.encode(x)
-    return x.contiguous().view(torch.uint8).reshape(-1)
-
-
-def _seq_decode(codecs, x):
-    for c in codecs[::-1]:
-        x = c.decode(x)
-    return x.contiguous().view(torch.uint8).reshape(-1)
+def _rows_u8(t, b):
+    return t.contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
 
 
 @pytest.mark.parametrize("name", list(_chains()))
-def test_encode_decode_chunks_rowwise(device, name):
+@pytest.mark.parametrize("n", [4096 * 3, 1000, 77])
+def test_encode_decode_chunks_vs_oracle(device, name, n):
+    """encode_chunks / decode_chunks: every row equals the oracle chain; the
+    chunk lengths cover whole tiles, ragged tails and a tiny chunk."""
     codecs, dtype = _chains()[name]
-    x = _make(dtype, 7, 4096 * 3, device, 1)
+    b = 7
+    x = _make(dtype, b, n, device, 1)
+    xh = x.cpu().numpy()
     enc = chunks.encode_chunks(codecs, x)
-    assert enc.shape[0] == 7
-    enc_u8 = enc.contiguous().view(torch.uint8).reshape(7, -1)
-    for i in range(7):
-        assert torch.equal(enc_u8[i], _seq_encode(codecs, x[i])), (name, i)
+    assert enc.shape[0] == b
+    enc_u8 = _rows_u8(enc, b)
+    for i in range(b):
+        ref = oracle_chain.chain_encode(codecs, xh[i])
+        assert enc_u8[i].tobytes() == ref, (name, n, i)
     dec = chunks.decode_chunks(codecs, enc)
-    dec_u8 = dec.contiguous().view(torch.uint8).reshape(7, -1)
-    for i in range(7):
-        assert torch.equal(dec_u8[i], _seq_decode(codecs, enc[i])), (name, i)
+    dec_u8 = _rows_u8(dec, b)
+    for i in range(b):
+        ref = oracle_chain.chain_decode(codecs, enc_u8[i].tobytes())
+        assert dec_u8[i].tobytes() == ref, (name, n, i)
 
 
 @pytest.mark.parametrize("name", ["bitround_shuffle_crc32", "quantize_shuffle_fletcher32", "astype_shuffle_jenkins"])
@@ -70,21 +75,30 @@ def test_decode_chunks_detects_corruption(device, name):
     enc = chunks.encode_chunks(codecs, x).clone()
     enc.view(torch.uint8)[3, 100] ^= 1
     with pytest.raises(RuntimeError):
+        oracle_chain.chain_decode(codecs, enc.view(torch.uint8)[3].cpu().numpy().tobytes())
+    with pytest.raises(RuntimeError):
         chunks.decode_chunks(codecs, enc)
 
 
-@pytest.mark.parametrize("name", ["bitround_shuffle_crc32", "fso_delta_shuffle_adler32", "delta_shuffle_crc32c"])
-def test_host_streamed_chunks(device, name):
+@pytest.mark.parametrize("name", ["bitround_shuffle_crc32", "fso_delta_shuffle_adler32", "delta_shuffle_crc32c",
+                                  "bitround_shuffle_fletcher32"])
+def test_host_streamed_chunks_vs_oracle(device, name):
+    """host_encode_chunks / host_decode_chunks (pinned slices through a ring of
+    device buffers on three streams): every row equals the oracle chain."""
     codecs, dtype = _chains()[name]
-    x = _make(dtype, 23, 4096 * 2, device, 3)
+    b = 23
+    x = _make(dtype, b, 4096 * 2, device, 3)
     host = x.cpu().pin_memory()
+    xh = host.numpy()
     enc_host = chunks.host_encode_chunks(codecs, host, slice_chunks=4, nslots=3)
-    enc_dev = chunks.encode_chunks(codecs, x).contiguous().view(torch.uint8).reshape(23, -1)
-    assert torch.equal(enc_host, enc_dev.cpu())
+    eh = enc_host.numpy()
+    for i in range(b):
+        assert eh[i].tobytes() == oracle_chain.chain_encode(codecs, xh[i]), (name, i)
     out = torch.empty_like(host).pin_memory()
     chunks.host_decode_chunks(codecs, enc_host, out, slice_chunks=5, nslots=2)
-    ref = chunks.decode_chunks(codecs, enc_dev).contiguous().view(torch.uint8).reshape(23, -1)
-    assert torch.equal(out.view(torch.uint8).reshape(23, -1), ref.cpu())
+    oh = out.view(torch.uint8).reshape(b, -1).numpy()
+    for i in range(b):
+        assert oh[i].tobytes() == oracle_chain.chain_decode(codecs, eh[i].tobytes()), (name, i)
 
 
 def test_host_decode_detects_corruption_after_stream(device):
@@ -95,3 +109,112 @@ def test_host_decode_detects_corruption_after_stream(device):
     out = torch.empty((9, 4096), dtype=torch.float32).pin_memory()
     with pytest.raises(RuntimeError, match="crc32 checksum do not match"):
         chunks.host_decode_chunks(codecs, enc, out, slice_chunks=2)
+
+
+# ---------------------------------------------------------------------------
+# batch-level entry points on padded rows (row stride > row bytes) and on
+# checksum rows of n + 4 bytes (4-B aligned when n % 4 == 0, unaligned else)
+# ---------------------------------------------------------------------------
+def _padded(device, b, n, pad, seed):
+    """[b, n] uint8 view of a [b, n + pad] buffer (padding bytes random)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    big = torch.randint(0, 256, (b, n + pad), generator=g, device=device, dtype=torch.uint8)
+    return big[:, :n]
+
+
+@pytest.mark.parametrize("n,pad", [(4096 * 4, 256), (4096 * 4, 4), (1000, 24), (65536 + 12, 4)])
+@pytest.mark.parametrize("es", [2, 4, 8])
+def test_shuffle_chunks_padded_vs_oracle(device, n, pad, es):
+    if n % es:
+        pytest.skip("Shuffle of a ragged element count is covered by the codec tests")
+    x = _padded(device, 9, n, pad, 5)
+    assert x.stride(0) == n + pad
+    xh = x.cpu().numpy()
+    out_big = torch.zeros((9, n + 8), dtype=torch.uint8, device=device)
+    enc = batch.shuffle_chunks(x, es, out=out_big[:, :n])
+    eh = out_big.cpu().numpy()
+    for i in range(9):
+        assert eh[i, :n].tobytes() == oracle.shuffle(xh[i], es).tobytes(), (n, pad, es, i)
+        assert not eh[i, n:].any(), "padding written"
+    dec = batch.unshuffle_chunks(enc, es)
+    dh = dec.cpu().numpy()
+    for i in range(9):
+        assert dh[i].tobytes() == oracle.unshuffle(eh[i, :n], es).tobytes()
+
+
+@pytest.mark.parametrize("n,pad", [(4096 * 4, 256), (4096, 4), (1002, 6), (3, 1)])
+def test_checksum_rows_padded_vs_oracle(device, n, pad):
+    """Fletcher32 / CRC32 / CRC32C / Adler32 batch encode into rows of n + 4
+    bytes (stride n + 4: 4-B aligned rows when n % 4 == 0) from padded input
+    rows; decode of those rows compacts the payloads; every row vs oracle."""
+    b = 11
+    x = _padded(device, b, n, pad, 6)
+    xh = x.cpu().numpy()
+    out = batch.fletcher32_encode_chunks(x)
+    assert out.stride(0) == n + 4
+    oh = out.cpu().numpy()
+    for i in range(b):
+        assert oh[i].tobytes() == oracle.fletcher32_encode(xh[i]), (n, i)
+    payloads, sums, stored = batch.fletcher32_decode_chunks(out)
+    ph = payloads.cpu().numpy()
+    assert torch.equal(sums, stored)
+    for i in range(b):
+        assert ph[i].tobytes() == xh[i].tobytes()
+    for cid in ("crc32", "crc32c", "adler32"):
+        for loc in ("start", "end"):
+            out = batch.checksum32_encode_chunks(x, cid, location=loc)
+            oh = out.cpu().numpy()
+            for i in range(b):
+                assert oh[i].tobytes() == oracle.checksum32_encode(cid, xh[i], loc).tobytes(), (cid, loc, n, i)
+            payloads, sums, stored = batch.checksum32_decode_chunks(out, cid, location=loc)
+            assert torch.equal(sums, stored), (cid, loc)
+            ph = payloads.cpu().numpy()
+            for i in range(b):
+                assert ph[i].tobytes() == oracle.checksum32_decode(cid, oh[i], loc).tobytes()
+
+
+@pytest.mark.parametrize("dt,at", [("<i2", "<i2"), ("<i4", "<i4"), ("<i8", "<i2"), ("<f4", "<f4"), ("<u2", "<u2")])
+def test_delta_chunks_padded_vs_oracle(device, dt, at):
+    """batch.delta_chunks on padded rows: each row its own Delta (first
+    element + running sum), delta.py:52-83, vs the oracle."""
+    d = Delta(dtype=dt, astype=at)
+    b, n = 6, 3001
+    isz, asz = np.dtype(dt).itemsize, np.dtype(at).itemsize
+    rng = np.random.default_rng(7)
+    if np.dtype(dt).kind == "f":
+        vals = np.cumsum(rng.integers(-4, 5, (b, n))).reshape(b, n).astype(dt)  # exact steps
+    else:
+        vals = rng.integers(-100, 100, (b, n)).astype(dt)
+    big = torch.zeros((b, n * isz + 40), dtype=torch.uint8, device=device)
+    big[:, : n * isz] = torch.from_numpy(vals.view(np.uint8).reshape(b, -1)).to(device)
+    x = big[:, : n * isz]
+    enc = batch.delta_chunks(x, d, encode=True)
+    eh = enc.cpu().numpy()
+    for i in range(b):
+        assert eh[i].tobytes() == oracle.delta_encode(vals[i], dt, at).tobytes(), (dt, at, i)
+    ebig = torch.zeros((b, n * asz + 24), dtype=torch.uint8, device=device)
+    ebig[:, : n * asz] = enc
+    dec = batch.delta_chunks(ebig[:, : n * asz], d, encode=False)
+    dh = dec.cpu().numpy()
+    for i in range(b):
+        assert dh[i].tobytes() == oracle.delta_decode(eh[i], dt, at).tobytes(), (dt, at, i)
+
+
+@pytest.mark.parametrize("es", [2, 4, 8])
+def test_shuffle_fletcher32_fused_rows_vs_oracle(device, es):
+    """The fused Shuffle + Fletcher32 batch (rows padded to encoded_stride)
+    and its fused verify + unshuffle: every row vs the oracle."""
+    b, n = 9, 8192 * es
+    x = _padded(device, b, n, 64, 8)
+    xh = x.cpu().numpy()
+    enc = batch.shuffle_fletcher32_encode_chunks(x, es)
+    assert enc.stride(0) == batch.encoded_stride(n)
+    eh = enc.cpu().numpy()
+    for i in range(b):
+        ref = oracle.fletcher32_encode(oracle.shuffle(xh[i], es))
+        assert eh[i, : n + 4].tobytes() == ref, (es, i)
+    dec, status = batch.fletcher32_unshuffle_decode_chunks(enc, n, es)
+    dh = dec.cpu().numpy()
+    for i in range(b):
+        assert dh[i].tobytes() == oracle.unshuffle(oracle.fletcher32_decode(eh[i, : n + 4]), es).tobytes()
+

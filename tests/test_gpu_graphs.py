@@ -1,8 +1,8 @@
-"""HIP-graph captured chains (numcodecs_amd.graphs.GraphChain): replaying
-the captured encode/decode must give the bytes of the eager chunk pipeline
-(tests/test_gpu_chunks.py pins that to the codecs applied one by one), for
-new inputs written into the captured buffer, and deferred checksum
-verification must still raise the codec's error."""
+"""HIP-graph captured chains (numcodecs_amd.graphs.GraphChain): every row of
+a replayed encode/decode must equal the ORACLE's codecs applied one after
+another to that chunk (tests/oracle_chain.py), for new inputs written into
+the captured buffer, and deferred checksum verification must still raise
+the codec's error."""
 
 import pytest
 import torch
@@ -11,6 +11,7 @@ from numcodecs_amd import (
     CRC32, CRC32C, Adler32, BitRound, Delta, FixedScaleOffset, Fletcher32, Quantize, Shuffle, chunks,
 )
 from numcodecs_amd.graphs import GraphChain
+from tests import oracle_chain
 
 pytestmark = pytest.mark.gpu
 
@@ -33,19 +34,22 @@ def _make(dtype, b, n, device, seed):
 
 
 @pytest.mark.parametrize("name", list(_chains()))
-def test_graph_chain_matches_eager(device, name):
+def test_graph_chain_vs_oracle(device, name):
     codecs, dtype = _chains()[name]
-    x0 = _make(dtype, 16, 16384, device, 1)
+    b = 16
+    x0 = _make(dtype, b, 16384, device, 1)
     genc = GraphChain(codecs, x0, "encode")
     for seed in (2, 3):  # replays on new data
-        x = _make(dtype, 16, 16384, device, seed)
-        ref = chunks.encode_chunks(codecs, x).contiguous().view(torch.uint8).reshape(16, -1)
-        got = genc(x).contiguous().view(torch.uint8).reshape(16, -1)
-        assert torch.equal(got, ref), (name, seed)
-    gdec = GraphChain(codecs, ref, "decode")
-    dref = chunks.decode_chunks(codecs, ref).contiguous().view(torch.uint8).reshape(16, -1)
-    dgot = gdec(ref).contiguous().view(torch.uint8).reshape(16, -1)
-    assert torch.equal(dgot, dref)
+        x = _make(dtype, b, 16384, device, seed)
+        xh = x.cpu().numpy()
+        got = genc(x).contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+        for i in range(b):
+            assert got[i].tobytes() == oracle_chain.chain_encode(codecs, xh[i]), (name, seed, i)
+    enc = torch.from_numpy(got.copy()).to(device)
+    gdec = GraphChain(codecs, enc, "decode")
+    dgot = gdec(enc).contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    for i in range(b):
+        assert dgot[i].tobytes() == oracle_chain.chain_decode(codecs, got[i].tobytes()), (name, i)
 
 
 def test_graph_decode_detects_corruption(device):

@@ -368,3 +368,40 @@ def test_cpu_baseline_workloads_roundtrip():
         w = cpu_baseline.Workload(cfg, nbytes, seed=3)
         w.step()
         w.verify()
+
+
+def test_oracle_chain_roundtrip():
+    """tests/oracle_chain.py (the pipeline tests' checker): each chain's oracle
+    encode decodes back to the input, and the checksum steps catch a flipped
+    byte -- on CPU, no device involved."""
+    from numcodecs_amd import (
+        CRC32, CRC32C, Adler32, AsType, BitRound, Delta, FixedScaleOffset, Fletcher32, JenkinsLookup3,
+        PackBits, Quantize, Shuffle,
+    )
+    from tests import oracle_chain
+
+    rng = np.random.default_rng(11)
+    f4 = (1000 + 10 * rng.random(3001)).astype("<f4")
+    f8 = f4.astype("<f8")
+    i4 = rng.integers(-1000, 1000, 3001).astype("<i4")
+    cases = [
+        ([BitRound(23), Shuffle(4), CRC32()], f4, True),
+        ([FixedScaleOffset(offset=1000, scale=1e3, dtype="<f4", astype="<i2"), Delta(dtype="<i2"), Shuffle(2),
+          Adler32(location="end")], f4, False),
+        ([Quantize(3, "<f8", "<f4"), Shuffle(4), Fletcher32()], f8, False),
+        ([AsType("<f4", "<f8"), Shuffle(4), JenkinsLookup3(initval=7)], f8, True),
+        ([Delta(dtype="<i4"), Shuffle(4), CRC32C()], i4, True),
+        ([PackBits()], rng.integers(0, 2, 77).astype(bool), True),
+    ]
+    for codecs, x, exact in cases:
+        enc = oracle_chain.chain_encode(codecs, x)
+        dec = np.frombuffer(oracle_chain.chain_decode(codecs, enc), dtype=x.dtype)
+        if exact:
+            assert np.array_equal(dec, x), codecs
+        else:
+            assert np.allclose(dec, x, atol=1e-2), codecs
+        if codecs[-1].codec_id in ("crc32", "crc32c", "adler32", "fletcher32", "jenkins_lookup3"):
+            bad = bytearray(enc)
+            bad[len(bad) // 2] ^= 1
+            with pytest.raises(RuntimeError):
+                oracle_chain.chain_decode(codecs, bytes(bad))

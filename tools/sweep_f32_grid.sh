@@ -1,10 +1,15 @@
 #!/usr/bin/env bash
-# One-launch Fletcher32 verify: sweep the block cap (MCODEC_F32_FUSED_GRID)
-# with tools/probe_verify_overhead.py; one JSON line per setting.
+# One-launch Fletcher32 verify: sweep its knobs (MCODEC_F32_FUSED_GRID,
+# MCODEC_F32_NTLD, MCODEC_F32_UNROLL, MCODEC_F32_SLICE_KB) with
+# tools/probe_verify_overhead.py; one JSON line per setting.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for g in 1024 2048 4096 8192; do
-  MCODEC_F32_FUSED_GRID=$g timeout -k 10 120 python tools/probe_verify_overhead.py >> gpurun_out/sweep_f32_grid.jsonl 2> gpurun_out/sweep_f32_grid.err || exit $?
+out=gpurun_out/sweep_f32_knobs.jsonl
+for cfg in "2048 1 4 32" "2048 0 4 32" "2048 1 8 32" "2048 0 8 32" "8192 0 4 32" "1024 0 8 64" "4096 0 8 16" "2048 0 1 32"; do
+  set -- $cfg
+  echo "{\"grid\": $1, \"ntld\": $2, \"unroll\": $3, \"slice_kb\": $4}" >> $out
+  MCODEC_F32_FUSED_GRID=$1 MCODEC_F32_NTLD=$2 MCODEC_F32_UNROLL=$3 MCODEC_F32_SLICE_KB=$4 \
+    timeout -k 10 120 python tools/probe_verify_overhead.py >> $out 2> gpurun_out/sweep_f32_knobs.err || exit $?
 done
-tail -4 gpurun_out/sweep_f32_grid.jsonl
+cat $out
