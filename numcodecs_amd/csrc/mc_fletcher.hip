@@ -34,30 +34,6 @@ MC_DEV void part_init(F32Part &p) { p.s1 = p.s2a = p.s2b = 0; p.nz = 0; }
 // the two big-endian words of a little-endian dword: w0 = bytes(0,1), w1 = bytes(2,3)
 MC_DEV uint32_t be_swap16x2(uint32_t x) { return mc_perm(0u, x, 0x02030001u); }
 
-// 16-B vector whose first word has weight c (= (n - j0) mod M)
-MC_DEV void part_vec(F32Part &p, mc_u32x4 v, uint32_t c) {
-  const uint32_t y0 = be_swap16x2(v.x), y1 = be_swap16x2(v.y);
-  const uint32_t y2 = be_swap16x2(v.z), y3 = be_swap16x2(v.w);
-  const uint32_t w0 = y0 & 0xffffu, w1 = y0 >> 16, w2 = y1 & 0xffffu, w3 = y1 >> 16;
-  const uint32_t w4 = y2 & 0xffffu, w5 = y2 >> 16, w6 = y3 & 0xffffu, w7 = y3 >> 16;
-  const uint32_t A = w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
-  const uint32_t B = w1 + 2 * w2 + 3 * w3 + 4 * w4 + 5 * w5 + 6 * w6 + 7 * w7;
-  p.s1 += A;
-  p.s2a += (uint64_t)c * A;
-  p.s2b += B;
-  p.nz |= v.x | v.y | v.z | v.w;
-}
-
-// one dword (two words) whose first word has weight c
-MC_DEV void part_dword(F32Part &p, uint32_t x, uint32_t c) {
-  const uint32_t y = be_swap16x2(x);
-  const uint32_t w0 = y & 0xffffu, w1 = y >> 16;
-  p.s1 += w0 + w1;
-  p.s2a += (uint64_t)c * (w0 + w1);
-  p.s2b += w1;
-  p.nz |= x;
-}
-
 // one word with weight c
 MC_DEV void part_word(F32Part &p, uint32_t w, uint32_t c) {
   p.s1 += w;
@@ -66,6 +42,58 @@ MC_DEV void part_word(F32Part &p, uint32_t w, uint32_t c) {
 }
 
 MC_DEV uint32_t mod_m(uint64_t x) { return (uint32_t)(x % M); }
+
+// A run of up to RUN_MAX consecutive 16-B vectors of one thread whose k-th
+// vector's first word has weight c0 - k*step (mod M).  Per vector only the
+// word sum A (a v_dot2_u32_u16 chain into the running prefix P) and the
+// intra-vector weighted sum B (a second chain) are accumulated, plus U += P;
+// the weights are applied once per run:
+//   sum_k c_k*A_k - B = c0*P - step*sum_k k*A_k - B,  sum_k k*A_k = k*P - U
+// (mod M).  13 VALU ops per vector against ~35 for unpacking the 8 words
+// and weighting each vector separately.
+constexpr uint32_t RUN_MAX = 64;  // keeps U < 2^31, B < 2^27
+typedef unsigned short f32_u16x2 __attribute__((ext_vector_type(2)));
+MC_DEV uint32_t dot2u(uint32_t a, uint32_t w, uint32_t c) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(f32_u16x2, a), __builtin_bit_cast(f32_u16x2, w), c, false);
+}
+struct F32Run {
+  uint32_t P, U, B, k, c0;
+};
+MC_DEV void run_start(F32Run &r, uint32_t c0) {
+  r.P = r.U = r.B = r.k = 0;
+  r.c0 = c0;
+}
+MC_DEV void run_vec(F32Run &r, mc_u32x4 v) {
+  const uint32_t y0 = be_swap16x2(v.x), y1 = be_swap16x2(v.y);
+  const uint32_t y2 = be_swap16x2(v.z), y3 = be_swap16x2(v.w);
+  uint32_t P = dot2u(y0, 0x00010001u, r.P);
+  P = dot2u(y1, 0x00010001u, P);
+  P = dot2u(y2, 0x00010001u, P);
+  P = dot2u(y3, 0x00010001u, P);
+  uint32_t B = dot2u(y0, 0x00010000u, r.B);  // words 0..7 weighted 0..7
+  B = dot2u(y1, 0x00030002u, B);
+  B = dot2u(y2, 0x00050004u, B);
+  B = dot2u(y3, 0x00070006u, B);
+  r.P = P;
+  r.U += P;
+  r.B = B;
+  ++r.k;
+}
+// fold the run into p (S1 exact, S2 mod M, nz) and start the next run at
+// weight c0 - k*step
+MC_DEV void run_fold(F32Part &p, F32Run &r, uint32_t step) {
+  if (!r.k) return;
+  const uint64_t P = r.P;
+  const uint64_t T2 = (uint64_t)r.k * P - r.U;  // sum_k k*A_k, exact
+  const uint32_t a = (uint32_t)(((uint64_t)r.c0 * (P % M)) % M);
+  const uint32_t t = (uint32_t)(((uint64_t)step * (T2 % M)) % M);
+  const uint32_t b = r.B % M;
+  p.s1 += P;
+  p.s2a += (a + 2 * M - t - b) % M;
+  p.nz |= (uint32_t)(P != 0);  // a word sum is 0 only if every word is
+  const uint32_t adv = (uint32_t)(((uint64_t)r.k * step) % M);
+  run_start(r, r.c0 >= adv ? r.c0 - adv : r.c0 + M - adv);
+}
 
 // reduce a thread's partial to {S1 mod M, S2 mod M, nz} across the block;
 // valid in thread 0.
@@ -186,6 +214,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     // weight of the vector's first word, stepped by 8*MC_BLOCK words per iteration
     uint32_t cw = (uint32_t)((nwords - 8 * (uint64_t)v) % M);
     constexpr uint32_t STEP = (8u * MC_BLOCK) % M;
+    F32Run r;
+    run_start(r, cw);
     // F32_UNROLL vectors in flight per thread before any is consumed
     for (; v + (F32_UNROLL - 1) * MC_BLOCK < v_hi; v += F32_UNROLL * MC_BLOCK) {
       mc_u32x4 x[F32_UNROLL];
@@ -194,16 +224,16 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
 #pragma unroll
       for (int j = 0; j < F32_UNROLL; ++j) {
         if constexpr (COPY) f32_st<AL>(d + (v + j * MC_BLOCK) * 16, x[j]);
-        part_vec(p, x[j], cw);
-        cw = cw >= STEP ? cw - STEP : cw + M - STEP;
+        run_vec(r, x[j]);
       }
+      if (r.k > RUN_MAX - F32_UNROLL) run_fold(p, r, STEP);
     }
     for (; v < v_hi; v += MC_BLOCK) {
       const mc_u32x4 x = f32_ld<AL>(s + v * 16);
       if constexpr (COPY) f32_st<AL>(d + v * 16, x);
-      part_vec(p, x, cw);
-      cw = cw >= STEP ? cw - STEP : cw + M - STEP;
+      run_vec(r, x);
     }
+    run_fold(p, r, STEP);
     if (sl == nslices - 1) {  // bytes after the last whole vector, word by word
       const size_t b0 = nvec * 16;
       for (size_t b = b0 + 2 * (size_t)threadIdx.x; b < nbytes; b += 2 * MC_BLOCK) {
@@ -316,12 +346,33 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_finalize(
 // fused Shuffle(es) + Fletcher32 over batches of chunks, one tile per block
 // (register layout of mc_shuffle.hip).  Needs count % TE == 0.
 // ---------------------------------------------------------------------------
-// weight of the dword at plane byte offset b*count + e (e even): word index
-// j = (b*count + e)/2; c = (nwords - j) mod M
-MC_DEV uint32_t plane_weight(uint32_t cb0, uint32_t cnt_m, int b, uint32_t extra) {
-  // cb0 = (nwords - e0/2) mod M; cnt_m = (count/2) mod M; extra < 2^20
-  const uint32_t x = cb0 + 32u * M - (uint32_t)b * cnt_m - extra;  // > 0 for b < 32
-  return x % M;
+// Per-thread accumulation over the plane dwords of a tile: the dword at plane
+// byte offset b*count + e (e even, quad q) is word j = (b*count + e)/2, with
+// weight c(q, b) = (nwords - j) mod M = cb0 - b*cnt_m - 2*MC_BLOCK*q (mod M)
+// (cb0 = (nwords - e0/2) mod M, cnt_m = (count/2) mod M), so sum c*A = cb0*SA - cnt_m*SbA - 2*MC_BLOCK*SqA (mod M)
+// with SA = sum A, SbA = sum b*A, SqA = sum q*A: four v_dot2_u32_u16 per
+// dword (b and q are compile-time constants) instead of a modulo and an
+// unpacking per dword.  Bounds: Q*ES <= 64 dwords per thread keeps every
+// sum below 2^29.
+struct PlaneSums {
+  uint32_t SA, SbA, SqA, SB;
+};
+MC_DEV void plane_init(PlaneSums &t) { t.SA = t.SbA = t.SqA = t.SB = 0; }
+MC_DEV void plane_dword(PlaneSums &t, uint32_t x, uint32_t b, uint32_t q) {
+  const uint32_t y = be_swap16x2(x);  // w0 in the low half, w1 in the high half
+  t.SA = dot2u(y, 0x00010001u, t.SA);
+  t.SbA = dot2u(y, b * 0x00010001u, t.SbA);
+  t.SqA = dot2u(y, q * 0x00010001u, t.SqA);
+  t.SB = dot2u(y, 0x00010000u, t.SB);  // the dword's second word: weight offset 1
+}
+MC_DEV void plane_fold(F32Part &p, const PlaneSums &t, uint32_t cb0, uint32_t cnt_m) {
+  constexpr uint32_t QW = (2u * MC_BLOCK) % M;
+  const uint64_t a = (uint64_t)cb0 * (t.SA % M) + (uint64_t)(M - cnt_m) * (t.SbA % M) +
+                     (uint64_t)(M - QW) * (t.SqA % M);
+  p.s1 += t.SA;
+  p.s2a += a % M;
+  p.s2b += t.SB;
+  p.nz |= (uint32_t)(t.SA != 0);
 }
 
 template <int ES, bool NT>
@@ -342,8 +393,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_f32_enc(
   uint32_t w[G::Q][ES];
 #pragma unroll
   for (int q = 0; q < G::Q; ++q) load_quad<ES, NT>(s + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w[q]);
-  F32Part p;
-  part_init(p);
+  static_assert(G::Q * ES <= 64, "PlaneSums bounds");
+  PlaneSums ps;
+  plane_init(ps);
 #pragma unroll
   for (int q = 0; q < G::Q; ++q) {
     uint32_t pl[ES];
@@ -351,9 +403,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_f32_enc(
 #pragma unroll
     for (int b = 0; b < ES; ++b) {
       mc_st4<NT>(d + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4, pl[b]);
-      part_dword(p, pl[b], plane_weight(cb0, cnt_m, b, 2u * MC_BLOCK * q));
+      plane_dword(ps, pl[b], b, q);
     }
   }
+  F32Part p;
+  part_init(p);
+  plane_fold(p, ps, cb0, cnt_m);
   uint32_t s1, s2, nz;
   block_reduce(p, s1, s2, nz);
   if (tid == 0) {
@@ -384,16 +439,20 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_unshuffle(
 #pragma unroll
     for (int q = 0; q < G::Q; ++q)
       p[q][b] = mc_ld4<NT>(s + (size_t)b * m.count + (size_t)(q * MC_BLOCK + tid) * 4);
-  F32Part acc;
-  part_init(acc);
+  static_assert(G::Q * ES <= 64, "PlaneSums bounds");
+  PlaneSums ps;
+  plane_init(ps);
 #pragma unroll
   for (int q = 0; q < G::Q; ++q) {
 #pragma unroll
-    for (int b = 0; b < ES; ++b) part_dword(acc, p[q][b], plane_weight(cb0, cnt_m, b, 2u * MC_BLOCK * q));
+    for (int b = 0; b < ES; ++b) plane_dword(ps, p[q][b], b, q);
     uint32_t w[ES];
     mc_planes_to_quad<ES>(p[q], w);
     store_quad<ES, NT>(d + (size_t)(q * MC_BLOCK + tid) * 4 * ES, w);
   }
+  F32Part acc;
+  part_init(acc);
+  plane_fold(acc, ps, cb0, cnt_m);
   uint32_t s1, s2, nz;
   block_reduce(acc, s1, s2, nz);
   if (tid == 0) {
