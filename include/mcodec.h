@@ -273,12 +273,16 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n,
                                 int dtype, int astype, double offset,
                                 double scale, mc_stream_t stream);
 /* Inverse chain: unshuffle, cumsum in astype, (x / scale + offset) in
- * float64 cast to dtype (fixedscaleoffset.py:99-113, delta.py:69-83). */
+ * float64 cast to dtype (fixedscaleoffset.py:99-113, delta.py:69-83).
+ * `ticket`: MC_ARRIVAL_WORDS device words (8-B aligned), zero before the
+ * first call and left zero (keep one per stream): the two-launch decode
+ * (scan folded into the passes); NULL: the three-pass scan.  Same bytes. */
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n);
 int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
                                 int astype, int dtype, double scale,
                                 double offset, void *workspace,
-                                size_t workspace_bytes, mc_stream_t stream);
+                                size_t workspace_bytes, uint32_t *ticket,
+                                mc_stream_t stream);
 
 /* ---- Checksum32 family (checksum32.py:45-209, jenkins.pyx:93-325) ------- */
 /* One 32-bit checksum per chunk of a batch (rows at src + c*src_stride):

@@ -116,7 +116,7 @@ _SIGNATURES = {
     "mc_fso_delta_shuffle_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp],
     "mc_fso_delta_shuffle_decode_workspace": [_c_size],
     "mc_fso_delta_shuffle_decode": [
-        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp,
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp, _c_vp,
     ],
     "mc_checksum32_workspace": [_c_int, _c_size, _c_size],
     "mc_checksum32_batch": [

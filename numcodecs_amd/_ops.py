@@ -102,6 +102,15 @@ class _VerifySlot:
 _VERIFY: "dict[tuple[int, int], _VerifySlot]" = {}
 
 
+def arrival_ticket(t: torch.Tensor, st: int):
+    """Device address of the stream's zeroed arrival counter (MC_ARRIVAL_WORDS
+    words, left zero by every kernel that takes it; stream order keeps the
+    users apart), or None during HIP-graph capture (the callers then take
+    their ticket-free schedules)."""
+    sl = _verify_slot(t, st)
+    return None if sl is None else sl.ticket.data_ptr()
+
+
 def _verify_slot(t: torch.Tensor, st: int):
     """The stream's verify slot, or None during HIP-graph capture."""
     if torch.cuda.is_current_stream_capturing():

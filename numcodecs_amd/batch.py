@@ -438,9 +438,11 @@ def _fso_delta_shuffle_decode(fso, delta, sh, x):
     _native.require_device()
     with torch.cuda.device(raw.device):
         ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_workspace(n), raw)
+        st = _ops.stream(raw)
         check(lib.mc_fso_delta_shuffle_decode(raw.data_ptr(), out.data_ptr(), n,
                                               _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype),
-                                              sc3, off4, ws.data_ptr(), ws.numel(), _ops.stream(raw)),
+                                              sc3, off4, ws.data_ptr(), ws.numel(),
+                                              _ops.arrival_ticket(raw, st), st),
               "mc_fso_delta_shuffle_decode")
     return out.view(torch_dtype(fso.dtype))
 

@@ -31,6 +31,7 @@ from . import _native, _ops
 __all__ = [
     "DBuf",
     "ensure_ndarray_like",
+    "is_ndarray_like",
     "ensure_ndarray",
     "ensure_contiguous_ndarray",
     "ensure_bytes",
@@ -77,14 +78,54 @@ def is_device_tensor(x) -> bool:
 # ---------------------------------------------------------------------------
 # host-side normalisation: the reference semantics, verbatim in behaviour
 # ---------------------------------------------------------------------------
+# DLPack device types of a HIP device array (dlpack.h: kDLCUDA = 2, kDLROCM = 10)
+_DL_DEVICE_TYPES = (2, 10)
+
+
+def _device_array_as_tensor(buf) -> "torch.Tensor | None":
+    """A zero-copy torch view of a NON-torch array living in HIP device memory
+    (CuPy-style ``__cuda_array_interface__`` or a DLPack producer whose
+    ``__dlpack_device__`` is a GPU), else None.  This is the device half of
+    the reference's NDArrayLike hook (ndarray_like.py:39-60,
+    compat.py:32-33: an ndarray-like object is used as it is)."""
+    dev = getattr(buf, "__dlpack_device__", None)
+    if dev is not None and hasattr(buf, "__dlpack__"):
+        try:
+            dtype_code = int(dev()[0])
+        except Exception:
+            return None
+        if dtype_code in _DL_DEVICE_TYPES:
+            return torch.from_dlpack(buf)
+        return None
+    if hasattr(buf, "__cuda_array_interface__"):
+        return torch.as_tensor(buf, device="cuda")
+    return None
+
+
+def is_ndarray_like(obj) -> bool:
+    """ndarray_like.py:39-64: True for objects with the ndarray attributes the
+    reference's NDArrayLike protocol lists (numpy arrays, CuPy-like device
+    arrays); torch tensors on a HIP device are accepted everywhere too."""
+    if isinstance(obj, (np.ndarray, torch.Tensor)):
+        return True
+    needed = ("dtype", "shape", "strides", "ndim", "size", "itemsize", "nbytes", "flags", "__len__",
+              "__getitem__", "__setitem__", "tobytes", "reshape", "view")
+    return all(hasattr(obj, a) for a in needed)
+
+
 def ensure_ndarray_like(buf):
-    """compat.py:9-41 -- a view of `buf` (numpy array or device tensor)."""
+    """compat.py:9-41 -- a view of `buf` (numpy array or device tensor).
+    Device arrays of other libraries (DLPack / ``__cuda_array_interface__``)
+    become zero-copy device tensors."""
     if is_device_tensor(buf):
         return buf
     if isinstance(buf, torch.Tensor):  # CPU tensor: the numpy view of it
         return buf.detach().numpy()
     if isinstance(buf, np.ndarray):
         return buf
+    dt = _device_array_as_tensor(buf)
+    if dt is not None:
+        return dt
     if isinstance(buf, array.array) and buf.typecode in "cu":
         raise TypeError("array.array with char or unicode type is not supported")
     return np.array(memoryview(buf), copy=False)
@@ -218,6 +259,10 @@ def to_dbuf(buf, *, flatten=True, contiguous=True) -> DBuf:
             and buf.is_contiguous()):
         # the common case (an encoded chunk): flat device bytes, used as they are
         return DBuf(buf, _U8, (buf.numel(),), "C", False)
+    if not isinstance(buf, (torch.Tensor, np.ndarray, bytes, bytearray, memoryview)):
+        dt = _device_array_as_tensor(buf)  # another library's device array: in place
+        if dt is not None:
+            buf = dt
     if is_device_tensor(buf):
         order = _tensor_order(buf)
         if order is None:

@@ -94,11 +94,13 @@ MC_DEV void c4_planes_to_deltas(const mc_u32x4 (&pl)[ES], uint32_t (&v)[C4_PER])
   }
 }
 
-template <int A, int ES>
+// NT: nontemporal loads (the 3-pass scan); the two-launch decode loads with
+// the default policy so that the apply pass's re-read hits the Infinity Cache
+template <int A, int ES, bool NT = true>
 MC_DEV void load16_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)[C4_PER]) {
   mc_u32x4 pl[ES];
 #pragma unroll
-  for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<true>(src + (size_t)b * n + e0);
+  for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<NT>(src + (size_t)b * n + e0);
   c4_planes_to_deltas<A, ES>(pl, v);
 }
 

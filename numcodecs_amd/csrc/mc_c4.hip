@@ -145,6 +145,145 @@ static void c4_decode(const uint8_t *s, uint8_t *d, uint64_t *sums, const C4Para
   k_c4_apply<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, pre, first, p);
 }
 
+// ---------------------------------------------------------------------------
+// Two-launch decode (the default when the caller passes an arrival `ticket`):
+// the scan of the tile totals is folded into the two passes, and the apply
+// pass's re-read of the encoded planes is partly served by the 256 MiB
+// Infinity Cache.
+//  * k_c4_reduce_g: a workgroup covers a PAIR of tiles (four 16-B loads per
+//    thread in flight, default-policy loads: the lines stay in the Infinity
+//    Cache for the apply pass), stores the two tile totals and adds the
+//    pair's total into its GROUP's word (GT tiles per group, at most 64
+//    groups) with ONE returning 64-bit atomic: word = (sum << 16) + count on
+//    the group's own 128-B line of `ticket` (the count never carries into the
+//    sum; sums are needed mod 2^32).  The group's last arriver writes
+//    gtot[g] and zeroes the word, so the ticket is left zero.
+//  * k_c4_apply_g: prefix of tile t = sum(gtot[0..g)) + the totals of the
+//    tiles of group g before t -- both loaded before the tile's data and
+//    folded into the block scan's one LDS round.
+// Measured on MI355X for n = 64 Mi (tools/probe_c4_2l.py, lab_mall.hip):
+// 95-99 us for the 3-pass scan (reduce 22, sums 6, apply 66) against
+// 83-86 us (reduce 25, apply 58: the temporal loads make about half the
+// re-read an Infinity-Cache hit; slabs that would make all of it one cost
+// more in launches than they saved).
+// ---------------------------------------------------------------------------
+constexpr unsigned C4_MAX_GROUPS = 64;
+
+static inline unsigned c4_group_tiles(size_t ntiles) {
+  unsigned gt = 256;  // tiles per group: at most 64 groups
+  while ((ntiles + gt - 1) / gt > C4_MAX_GROUPS) gt *= 2;
+  return gt;
+}
+
+template <int D, int A>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_reduce_g(const uint8_t *__restrict__ src, uint32_t *ws,
+                                                         uint32_t *ticket, C4Params p, size_t ntiles, unsigned GT) {
+  constexpr int ES = c4_es<A>();
+  __shared__ uint32_t lds[2][MC_BLOCK / 64];
+  uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t t0 = (size_t)blockIdx.x * 2;
+  const size_t e0 = t0 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t acc[2] = {0, 0};
+  uint32_t v[2][C4_PER];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) load16_deltas<A, ES, false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    acc[0] += __shfl_xor(acc[0], off, 64);
+    acc[1] += __shfl_xor(acc[1], off, 64);
+  }
+  if (lane == 0) {
+    lds[0][wave] = acc[0];
+    lds[1][wave] = acc[1];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t tot = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t a = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) a += lds[h][w];
+    if (t0 + h < ntiles) tile_tot[t0 + h] = a;
+    tot += a;
+  }
+  const size_t g = t0 / GT;
+  const size_t in_group = ntiles - g * GT < GT ? ntiles - g * GT : GT;
+  const unsigned long long arrivals = (in_group + 1) / 2;  // workgroups (pairs) of group g
+  unsigned long long *word = reinterpret_cast<unsigned long long *>(ticket + (size_t)MC_ARRIVAL_LINE * g);
+  const unsigned long long old = atomicAdd(word, ((unsigned long long)tot << 16) | 1ull);
+  if ((old & 0xffffu) + 1u == arrivals) {
+    gtot[g] = (uint32_t)(old >> 16) + tot;
+    *word = 0;  // every arrival of this call is in: left zero
+  }
+}
+
+template <int D, int A>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_apply_g(const uint8_t *__restrict__ src,
+                                                        uint8_t *__restrict__ dst, const uint32_t *ws, C4Params p,
+                                                        size_t ntiles, unsigned GT) {
+  constexpr int DS = D == MC_F4 ? 4 : 8;
+  constexpr int ES = c4_es<A>();
+  __shared__ uint32_t red[2][MC_BLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
+  const uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const size_t tile = blockIdx.x;
+  const size_t g = tile / GT, gt0 = g * GT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // prefix pieces first (their loads overlap the data loads below)
+  uint32_t x = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;
+  for (unsigned j = threadIdx.x; j < GT && gt0 + j < tile; j += MC_BLOCK) x += tile_tot[gt0 + j];
+  uint32_t v[C4_PER];
+  const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  if (e0 < p.n) {
+    load16_deltas<A, ES, false>(src, p.n, e0, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+  }
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < C4_PER; ++k) {
+    run += v[k];
+    v[k] = run;
+  }
+  // one LDS round: the exclusive scan of `run` and the block sum of `x`
+  uint32_t incl = run;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  if (lane == 63) red[0][wave] = incl;
+  if (lane == 0) red[1][wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) {
+    if (w < wave) pre += red[0][w];
+    pre += red[1][w];
+  }
+  c4_finish<D, A>(dst, tile, v, pre + (incl - run), outb, p);
+}
+
+template <int D, int A>
+static void c4_decode_g(const uint8_t *s, uint8_t *d, uint32_t *ws, uint32_t *ticket, const C4Params &p,
+                        hipStream_t st) {
+  const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const unsigned gt = c4_group_tiles(ntiles);
+  k_c4_reduce_g<D, A><<<(unsigned)((ntiles + 1) / 2), MC_BLOCK, 0, st>>>(s, ws, ticket, p, ntiles, gt);
+  k_c4_apply_g<D, A><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, ws, p, ntiles, gt);
+}
+
 }  // namespace
 
 extern "C" {
@@ -168,21 +307,32 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
 
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n) {
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  return 24 * ((ntiles + 1) / 2);  // pair totals, first values, pair prefixes
+  const size_t three_pass = 24 * ((ntiles + 1) / 2);  // pair totals, first values, pair prefixes
+  const size_t two_launch = 4 * (ntiles + C4_MAX_GROUPS);  // tile totals, group totals
+  return three_pass > two_launch ? three_pass : two_launch;
 }
 
 int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n, int astype, int dtype,
                                 double scale, double offset, void *workspace,
-                                size_t workspace_bytes, mc_stream_t stream) {
+                                size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
   if (n == 0) return MC_OK;
   if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
   if (!workspace || workspace_bytes < mc_fso_delta_shuffle_decode_workspace(n)) return MC_ENOSPC;
+  if (ticket && (uintptr_t)ticket % 8) return MC_EINVAL;
   const C4Params p = c4_decode_params(n, scale, offset);
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
-  uint64_t *sums = static_cast<uint64_t *>(workspace);
   hipStream_t st = (hipStream_t)stream;
-  MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  // the two-launch decode needs a ticket and groups of at most 1024 tiles
+  // (the apply workgroup sums its group's earlier tile totals, 4 per thread)
+  if (ticket && c4_group_tiles(ntiles) <= 1024) {
+    uint32_t *ws = static_cast<uint32_t *>(workspace);
+    MC_C4_DISPATCH(c4_decode_g, s, d, ws, ticket, p, st);
+  } else {
+    uint64_t *sums = static_cast<uint64_t *>(workspace);
+    MC_C4_DISPATCH(c4_decode, s, d, sums, p, st);
+  }
   return mc_last_launch();
 }
 

@@ -207,3 +207,15 @@ def test_next_codecs_config():
         with pytest.raises(ValueError):
             cls(location="foo")
     assert JenkinsLookup3(prefix=b"ab").prefix.tolist() == [97, 98]
+
+
+def test_is_ndarray_like_mirrors_reference_protocol():
+    """ndarray_like.py:39-64: the structural NDArrayLike check."""
+    import numpy as np
+
+    from numcodecs_amd.compat import is_ndarray_like
+
+    assert is_ndarray_like(np.zeros(3))
+    assert not is_ndarray_like(b"abc")
+    assert not is_ndarray_like(bytearray(3))
+    assert not is_ndarray_like(memoryview(b"abc"))

@@ -155,3 +155,40 @@ def test_fso_decode_every_int16(device, dt, scale):
     with np.errstate(all="ignore"):
         ref = oracle.fso_decode(a, -7.125, scale, dt, "<i2")
     assert dec.view(np.uint8).tobytes() == np.ascontiguousarray(ref).view(np.uint8).tobytes(), scale
+
+
+@pytest.mark.parametrize("dt,at,n", [("<f4", "<i2", 4096 * 300 + 16), ("<f8", "<u4", 256 * 4096 * 7 + 4096 * 3 + 16),
+                                     ("<f4", "<u2", 4096 * 16384 + 4096 * 601 + 32), ("<f4", "<i4", 64)])
+def test_two_launch_decode_vs_oracle(device, dt, at, n):
+    """The default decode (two launches: group totals by one 64-bit arrival
+    atomic per tile pair, prefixes folded into the apply pass) against the
+    oracle chain and the three-pass scan (the lab's variant 1 = the product
+    with no ticket): one group and many, a partial last group, an odd tile
+    count, groups of 512 tiles (n > 64 Mi); the stream's ticket is left zero."""
+    from numcodecs_amd import _ops
+    from numcodecs_amd._native import check, lib
+
+    rng = np.random.default_rng(n)
+    x = (1000.0 + rng.uniform(-15, 15, n)).astype(dt)
+    scale = 1e3 if np.dtype(at).itemsize == 2 else 1e6
+    codecs = _chain(dt, at, 1000, scale)
+    pipe = batch.FilterPipeline(codecs)
+    xd = torch.from_numpy(x).to(device)
+    enc = pipe.encode(xd)
+    dec = pipe.decode(enc)
+    eh = enc.cpu().numpy()
+    with np.errstate(all="ignore"):
+        ref = oracle.fso_decode(oracle.delta_decode(oracle.unshuffle(eh, np.dtype(at).itemsize), at), 1000,
+                                scale, dt, at)
+    assert np.array_equal(dec.cpu().numpy().view(np.uint8), ref.view(np.uint8))
+    lab = lab_lib()
+    _, _, sc3, off4 = batch._c4_scalars(*codecs)
+    raw = enc.view(torch.uint8)
+    out = torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, device=device)
+    ws = torch.empty(lib.mc_fso_delta_shuffle_decode_workspace(n), dtype=torch.uint8, device=device)
+    check(lab.mc_lab_c4_decode_variant(raw.data_ptr(), out.data_ptr(), n, _ops.dtype_code(at), _ops.dtype_code(dt),
+                                       sc3, off4, ws.data_ptr(), ws.numel(), 1, _ops.stream(raw)), "three-pass")
+    assert torch.equal(out, dec.view(torch.uint8).reshape(-1))
+    st = _ops.stream(raw)
+    torch.cuda.synchronize()
+    assert not _ops._verify_slot(raw, st).ticket.any()

@@ -550,3 +550,45 @@ def test_single_chunk_verify_one_launch(device, codec_id):
     torch.cuda.synchronize()
     for sl in _ops._VERIFY.values():
         assert not sl.ticket.any()
+
+
+class _DLPackDeviceArray:
+    """A non-torch device array as another library would hand it over: only
+    the DLPack producer protocol (ndarray_like.py:39-60 / compat.py:32-33 of
+    the reference accept any ndarray-like object as it is)."""
+
+    def __init__(self, t):
+        self._t = t
+
+    def __dlpack__(self, stream=None):
+        return self._t.__dlpack__()
+
+    def __dlpack_device__(self):
+        return self._t.__dlpack_device__()
+
+
+class _CAIDeviceArray:
+    """The same through ``__cuda_array_interface__`` (CuPy-style)."""
+
+    def __init__(self, t):
+        self._t = t
+        self.__cuda_array_interface__ = t.__cuda_array_interface__
+
+
+def test_foreign_device_arrays_are_used_in_place(device):
+    """Device arrays of other libraries (DLPack / __cuda_array_interface__)
+    encode on the device, without a host round trip, to the oracle's bytes."""
+    from numcodecs_amd import Delta
+    from numcodecs_amd.compat import ensure_ndarray_like
+
+    x = torch.randn(4096 * 3, device=device)
+    xh = x.cpu().numpy()
+    for wrap in (_DLPackDeviceArray, _CAIDeviceArray):
+        obj = wrap(x)
+        view = ensure_ndarray_like(obj)
+        assert isinstance(view, torch.Tensor) and view.data_ptr() == x.data_ptr()
+        enc = Shuffle(4).encode(obj)
+        assert isinstance(enc, torch.Tensor) and enc.is_cuda
+        assert np.array_equal(enc.cpu().numpy(), oracle.shuffle(xh, 4))
+        d = Delta(dtype="<f4")
+        assert np.array_equal(d.encode(obj).cpu().numpy().view("<f4"), oracle.delta_encode(xh, "<f4"))

@@ -4,7 +4,8 @@
 // FSO -> Delta -> Shuffle(2) chunk pipeline that DESIGN.md measured against
 // the product's 3-pass scan and rejected, kept so the measurement can be
 // repeated and so their byte-identity stays tested (tests/test_gpu_c4.py):
-//   1  the product's three-pass scan (= 0)
+//   1  the product's three-pass scan (= 0; the product's default is the
+//      two-launch decode, mc_fso_delta_shuffle_decode with a ticket)
 //   2  single-pass decoupled look-back, tiles numbered by an atomic counter
 //   3  single-pass look-back in workgroup (blockIdx) order
 //   4  = 3 with every wait replaced by the data-derived prefix fallback
@@ -234,7 +235,7 @@ int mc_lab_c4_decode_variant(const void *src, void *dst, size_t n, int astype, i
   if (variant < 0 || variant > 7) return MC_EINVAL;
   if (variant <= 1)
     return mc_fso_delta_shuffle_decode(src, dst, n, astype, dtype, scale, offset, workspace, workspace_bytes,
-                                       stream);
+                                       nullptr, stream);
   if (n == 0) return MC_OK;
   if (!c4_ok(src, dst, n, dtype, astype)) return MC_EINVAL;
   if (!workspace || workspace_bytes < mc_lab_c4_decode_workspace(n)) return MC_ENOSPC;

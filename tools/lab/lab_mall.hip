@@ -1,0 +1,305 @@
+// lab_mall.hip -- LAB ONLY (libmcodec_lab.so).  Does the three-pass C4
+// decode's second read of the encoded planes come from the 256 MB Infinity
+// Cache (MALL) when the two passes walk the chunk in OPPOSITE orders?
+//
+// The product's reduce and apply passes both walk tiles in increasing order,
+// so the apply pass re-reads tile t after the reduce pass has read every
+// other tile and the apply pass has moved 3x as much again: a reuse distance
+// larger than the MALL for most of the chunk.  With the reduce pass walking
+// the tiles from the END (blockIdx -> last tile first; workgroups are
+// dispatched in blockIdx order), the tiles the apply pass needs first are the
+// ones the reduce pass read last.  flags:
+//   bit 0  reduce pass in reverse tile order
+//   bit 1  reduce pass with default-policy (temporal) loads instead of nt
+//   bit 2  apply pass with default-policy loads
+//   bit 3  apply pass in reverse tile order
+// FixedScaleOffset(f4 <- i2) <- Delta(i2) <- Shuffle(2) only (the BASELINE C4
+// config); identical bytes to mc_fso_delta_shuffle_decode for every flag.
+#include "mc_c4.h"
+
+namespace {
+
+template <bool NT>
+MC_DEV void mall_load_deltas(const uint8_t *src, size_t n, size_t e0, uint32_t (&v)[C4_PER]) {
+  mc_u32x4 pl[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) pl[b] = mc_ld16<NT>(src + (size_t)b * n + e0);
+  c4_planes_to_deltas<MC_I2, 2>(pl, v);
+}
+
+template <bool REV, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_mall_reduce2(const uint8_t *__restrict__ src,
+                                                          uint64_t *__restrict__ pair_sums,
+                                                          uint64_t *__restrict__ first, C4Params p) {
+  __shared__ uint64_t lds[2][MC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t pair = REV ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const size_t e0 = pair * 2 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t acc[2] = {0, 0};
+  uint32_t v[2][C4_PER];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<NT>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    acc[0] += __shfl_xor(acc[0], off, 64);
+    acc[1] += __shfl_xor(acc[1], off, 64);
+  }
+  if (lane == 0) {
+    lds[0][wave] = acc[0];
+    lds[1][wave] = acc[1];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, b = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) {
+      a += (uint32_t)lds[0][w];
+      b += (uint32_t)lds[1][w];
+    }
+    first[pair] = a;
+    pair_sums[pair] = (uint32_t)(a + b);
+  }
+}
+
+template <bool REV, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_mall_apply(const uint8_t *__restrict__ src,
+                                                        uint8_t *__restrict__ dst,
+                                                        const uint64_t *__restrict__ pair_pre,
+                                                        const uint64_t *__restrict__ first, C4Params p) {
+  __shared__ uint32_t red[MC_BLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * 4];
+  const size_t tile = REV ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  uint32_t v[C4_PER];
+  const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  if (e0 < p.n) {
+    mall_load_deltas<NT>(src, p.n, e0, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+  }
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < C4_PER; ++k) {
+    run += v[k];
+    v[k] = run;
+  }
+  uint32_t agg;
+  const uint32_t excl = mc_block_excl_scan32(run, red, &agg);
+  const uint32_t tile_pre = (uint32_t)pair_pre[tile >> 1] + ((tile & 1) ? (uint32_t)first[tile >> 1] : 0u);
+  c4_finish<MC_F4, MC_I2>(dst, tile, v, tile_pre + excl, outb, p);
+}
+
+template <bool R_REV, bool R_NT>
+void launch_reduce(unsigned g, const uint8_t *s, uint64_t *pair, uint64_t *first, const C4Params &p,
+                   hipStream_t st) {
+  k_mall_reduce2<R_REV, R_NT><<<g, MC_BLOCK, 0, st>>>(s, pair, first, p);
+}
+template <bool A_REV, bool A_NT>
+void launch_apply(unsigned g, const uint8_t *s, uint8_t *d, const uint64_t *pre, const uint64_t *first,
+                  const C4Params &p, hipStream_t st) {
+  k_mall_apply<A_REV, A_NT><<<g, MC_BLOCK, 0, st>>>(s, d, pre, first, p);
+}
+
+
+// ---------------------------------------------------------------------------
+// Two-launch decode: the scan of the tile totals is folded into the passes.
+// A reduce workgroup covers R consecutive tiles (2*R 16-B loads per thread in
+// flight), stores the R tile totals and adds its total into its GROUP's word
+// (GT tiles per group, at most 64 groups) with ONE returning 64-bit atomic:
+// word = (sum << 16) + count, on its own `tstride`-word slot of `ticket`
+// (the count never carries into the sum; the sum is needed mod 2^32).  The
+// group's last arriver writes gtot[g] and zeroes the word (left zero).  An
+// apply workgroup takes its prefix as sum(gtot[0..g)) + sum(tile totals of
+// group g before its tile) -- both loaded before its data, folded into the
+// block scan's one LDS round.
+// ---------------------------------------------------------------------------
+template <int R, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4r_reduce(const uint8_t *__restrict__ src, uint32_t *ws,
+                                                        uint32_t *ticket, C4Params p, size_t wg0, size_t ntiles,
+                                                        unsigned GT, unsigned tstride) {
+  __shared__ uint32_t lds[R][MC_BLOCK / 64];
+  uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t t0 = (wg0 + blockIdx.x) * R;
+  const size_t e0 = t0 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t acc[R];
+  uint32_t v[R][C4_PER];
+#pragma unroll
+  for (int h = 0; h < R; ++h)
+    if (e0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<NT>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+  for (int h = 0; h < R; ++h) {
+    acc[h] = 0;
+    if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int h = 0; h < R; ++h) acc[h] += __shfl_xor(acc[h], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int h = 0; h < R; ++h) lds[h][wave] = acc[h];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t tot = 0;
+#pragma unroll
+  for (int h = 0; h < R; ++h) {
+    uint32_t a = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) a += lds[h][w];
+    if (t0 + h < ntiles) tile_tot[t0 + h] = a;
+    tot += a;
+  }
+  const size_t g = t0 / GT;
+  const size_t wgs_in_group = ((ntiles - g * GT < GT ? ntiles - g * GT : GT) + R - 1) / R;
+  unsigned long long *word = reinterpret_cast<unsigned long long *>(ticket + (size_t)tstride * g);
+  const unsigned long long old = atomicAdd(word, ((unsigned long long)tot << 16) | 1ull);
+  if ((old & 0xffffu) + 1u == wgs_in_group) {
+    gtot[g] = (uint32_t)(old >> 16) + tot;
+    *word = 0;
+  }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4r_apply(const uint8_t *__restrict__ src,
+                                                       uint8_t *__restrict__ dst, const uint32_t *ws,
+                                                       C4Params p, size_t tile0, size_t ntiles, unsigned GT) {
+  __shared__ uint32_t red[2][MC_BLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * 4];
+  const uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const size_t tile = tile0 + blockIdx.x;
+  const size_t g = tile / GT, gt0 = g * GT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // prefix pieces first (their loads overlap the data loads below)
+  uint32_t x = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;
+  for (unsigned j = threadIdx.x; j < GT; j += MC_BLOCK)
+    if (gt0 + j < tile) x += tile_tot[gt0 + j];
+  uint32_t v[C4_PER];
+  const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  if (e0 < p.n) {
+    mall_load_deltas<NT>(src, p.n, e0, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+  }
+  uint32_t run = 0;
+#pragma unroll
+  for (int k = 0; k < C4_PER; ++k) {
+    run += v[k];
+    v[k] = run;
+  }
+  // one LDS round: the exclusive scan of `run` and the block sum of `x`
+  uint32_t incl = run;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  if (lane == 63) red[0][wave] = incl;
+  if (lane == 0) red[1][wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) {
+    if (w < wave) pre += red[0][w];
+    pre += red[1][w];
+  }
+  c4_finish<MC_F4, MC_I2>(dst, tile, v, pre + (incl - run), outb, p);
+}
+
+template <bool NT>
+void launch_c4r_reduce(int R, unsigned grid, const uint8_t *s, uint32_t *ws, uint32_t *ticket, const C4Params &p,
+                       size_t wg0, size_t ntiles, unsigned GT, unsigned ts, hipStream_t st) {
+  if (R == 2) k_c4r_reduce<2, NT><<<grid, MC_BLOCK, 0, st>>>(s, ws, ticket, p, wg0, ntiles, GT, ts);
+  else if (R == 4) k_c4r_reduce<4, NT><<<grid, MC_BLOCK, 0, st>>>(s, ws, ticket, p, wg0, ntiles, GT, ts);
+  else k_c4r_reduce<8, NT><<<grid, MC_BLOCK, 0, st>>>(s, ws, ticket, p, wg0, ntiles, GT, ts);
+}
+
+}  // namespace
+
+extern "C" {
+
+// FSO(f4 <- i2) <- Delta(i2) <- Shuffle(2) decode of n elements with the
+// pass orders / load policies of `flags` (above); workspace as for
+// mc_fso_delta_shuffle_decode.
+int mc_lab_c4_decode_mall(const void *src, void *dst, size_t n, double scale, double offset, void *workspace,
+                          size_t workspace_bytes, int flags, mc_stream_t stream) {
+  if (n == 0) return MC_OK;
+  if (!c4_ok(src, dst, n, MC_F4, MC_I2)) return MC_EINVAL;
+  if (!workspace || workspace_bytes < mc_fso_delta_shuffle_decode_workspace(n)) return MC_ENOSPC;
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const size_t npairs = (ntiles + 1) / 2;
+  uint64_t *sums = static_cast<uint64_t *>(workspace);
+  uint64_t *pair = sums, *first = sums + npairs, *pre = sums + 2 * npairs;
+  const unsigned gp = (unsigned)npairs, gt = (unsigned)ntiles;
+  switch (flags & 3) {  // bit 1 set = temporal = NT false
+    case 0: launch_reduce<false, true>(gp, s, pair, first, p, st); break;
+    case 1: launch_reduce<true, true>(gp, s, pair, first, p, st); break;
+    case 2: launch_reduce<false, false>(gp, s, pair, first, p, st); break;
+    default: launch_reduce<true, false>(gp, s, pair, first, p, st); break;
+  }
+  mc_launch_scan_sums_mw<false>(pair, pre, npairs, st);
+  switch ((flags >> 2) & 3) {  // bit 2 = temporal, bit 3 = reverse
+    case 0: launch_apply<false, true>(gt, s, d, pre, first, p, st); break;
+    case 1: launch_apply<false, false>(gt, s, d, pre, first, p, st); break;
+    case 2: launch_apply<true, true>(gt, s, d, pre, first, p, st); break;
+    default: launch_apply<true, false>(gt, s, d, pre, first, p, st); break;
+  }
+  return mc_last_launch();
+}
+
+// Two-launch decode (above) in `nslabs` slabs; flags: bit 1 reduce with
+// default-policy loads, bit 2 apply with default-policy loads, bits 4-5
+// log2(R) (0 -> R = 4), bits 8-: the group words' stride in uint32 words
+// (0 -> one 128-B line).  `ticket`: 64 strides of zeroed words, left zero.
+size_t mc_lab_c4_2l_workspace(size_t n) {  // tile totals + 64 group totals
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  return (ntiles + 64) * sizeof(uint32_t);
+}
+
+int mc_lab_c4_decode_2l(const void *src, void *dst, size_t n, double scale, double offset, void *workspace,
+                        size_t workspace_bytes, uint32_t *ticket, int flags, int nslabs, mc_stream_t stream) {
+  if (n == 0) return MC_OK;
+  if (!c4_ok(src, dst, n, MC_F4, MC_I2) || !ticket || nslabs < 1) return MC_EINVAL;
+  if (!workspace || workspace_bytes < mc_lab_c4_2l_workspace(n)) return MC_ENOSPC;
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const int lr = (flags >> 4) & 3;
+  const int R = lr ? 1 << lr : 4;
+  unsigned GT = 256;  // tiles per group: at most 64 groups, at most 1024 tiles per group
+  while ((ntiles + GT - 1) / GT > 64) GT *= 2;
+  if (GT > 1024) return MC_EINVAL;
+  const size_t ngroups = (ntiles + GT - 1) / GT;
+  const unsigned ts = (flags >> 8) ? (unsigned)(flags >> 8) : MC_ARRIVAL_LINE;
+  uint32_t *ws = static_cast<uint32_t *>(workspace);
+  for (int sl = 0; sl < nslabs; ++sl) {
+    const size_t g0 = ngroups * sl / nslabs, g1 = ngroups * (sl + 1) / nslabs;
+    if (g1 == g0) continue;
+    const size_t t0 = g0 * GT, t1 = g1 * GT < ntiles ? g1 * GT : ntiles;
+    const unsigned grid = (unsigned)((t1 - t0 + R - 1) / R);
+    if (flags & 2) launch_c4r_reduce<false>(R, grid, s, ws, ticket, p, t0 / R, ntiles, GT, ts, st);
+    else launch_c4r_reduce<true>(R, grid, s, ws, ticket, p, t0 / R, ntiles, GT, ts, st);
+    if (flags & 4) k_c4r_apply<false><<<(unsigned)(t1 - t0), MC_BLOCK, 0, st>>>(s, d, ws, p, t0, ntiles, GT);
+    else k_c4r_apply<true><<<(unsigned)(t1 - t0), MC_BLOCK, 0, st>>>(s, d, ws, p, t0, ntiles, GT);
+  }
+  return mc_last_launch();
+}
+
+}  // extern "C"
