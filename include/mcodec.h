@@ -139,9 +139,13 @@ int mc_delta_encode(const void *src, void *dst, size_t n, int dtype,
  * decode is the serial chain.  The workspace's last 8 bytes hold the index
  * of the first mismatch (n if none) after the call. */
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
+/* `ticket`: MC_ARRIVAL_WORDS device words (8-B aligned), zero before the
+ * first call and left zero (one per stream): same-width integer decodes of
+ * 1/2/4-byte elements run as two launches (tile-total scan folded into the
+ * passes); NULL: the three-pass scan.  Same bytes either way. */
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype,
                     int dtype, void *workspace, size_t workspace_bytes,
-                    mc_stream_t stream);
+                    uint32_t *ticket, mc_stream_t stream);
 /* Batched Delta over nchunks chunks of n elements each (chunk c read at
  * src + c*src_stride, written at dst + c*dst_stride; strides in bytes).
  * Each chunk is an independent Delta (its own first element / cumsum).

@@ -82,7 +82,7 @@ _SIGNATURES = {
     "mc_bitround_shuffle": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_workspace": [_c_size, _c_int, _c_int],
-    "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp],
+    "mc_delta_decode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp, _c_size, _c_vp, _c_vp],
     "mc_delta_encode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch": [_c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_vp],
     "mc_delta_decode_batch_workspace": [_c_size, _c_size, _c_int, _c_int],

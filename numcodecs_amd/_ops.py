@@ -218,8 +218,9 @@ def delta_decode(src, dst, n, astype, dtype) -> None:
         a, d = dtype_code(astype), dtype_code(dtype)
         ws_n = lib.mc_delta_decode_workspace(n, a, d)
         ws = workspace(ws_n, src)
+        st = stream(src)
         check(lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d, ws.data_ptr(), ws.numel(),
-                                  stream(src)), "mc_delta_decode")
+                                  arrival_ticket(src, st), st), "mc_delta_decode")
 
 
 def _scalar_args(value, dt):

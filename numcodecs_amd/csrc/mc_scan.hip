@@ -448,11 +448,11 @@ constexpr size_t ds_tile() { return (size_t)ds_per<ES>() * MC_BLOCK; }
 
 // the values of elements [e0, e0 + PER/2) (one 16-B vector; zeros past n)
 // into v[at .. at + PER/2)
-template <int ES>
+template <int ES, bool NT = true>
 MC_DEV void ds_load_half(const uint8_t *src, size_t n, size_t e0, dacc_t<ES> (&v)[ds_per<ES>()], int at) {
   constexpr int H = ds_per<ES>() / 2;
   if (e0 + H <= n) {
-    const mc_u32x4 w = mc_ld16<true>(src + e0 * ES);
+    const mc_u32x4 w = mc_ld16<NT>(src + e0 * ES);
     const uint32_t d[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int i = 0; i < H; ++i) {
@@ -700,6 +700,176 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_rows(const uint8_t *__restri
     ds_store_half<ES>(dst, n, base + ob, v, H);
     carry += ta + tb;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Two-launch same-width decode (ES <= 4, with an arrival ticket): the scan of
+// the tile totals folded into the passes, as for the C4 decode (mc_c4.hip,
+// k_c4_reduce_g / k_c4_apply_g).  A reduce workgroup covers DS_GROUP tiles
+// (default-policy loads: the apply pass re-reads them partly from the
+// Infinity Cache), stores their totals and adds its total into its group's
+// word with one returning 64-bit atomic, word = (sum << 16) + count (sums
+// mod 2^32 suffice for ES <= 4); the group's last arriver writes gtot[g] and
+// zeroes the word.  The apply workgroup's prefix = sum(gtot[0..g)) + the
+// totals of its group's earlier tiles, loaded before its data.
+// ---------------------------------------------------------------------------
+constexpr unsigned DS_MAX_GROUPS = 64;
+
+static inline unsigned ds_group_tiles(size_t ntiles) {
+  unsigned gt = 256;  // tiles per group (a multiple of DS_GROUP): at most 64 groups
+  while ((ntiles + gt - 1) / gt > DS_MAX_GROUPS) gt *= 2;
+  return gt;
+}
+
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce_g(const uint8_t *__restrict__ src, size_t n,
+                                                            uint32_t *ws, uint32_t *ticket, size_t ntiles,
+                                                            unsigned GT) {
+  static_assert(ES <= 4, "group sums are kept mod 2^32");
+  constexpr int PER = ds_per<ES>();
+  constexpr size_t TE = ds_tile<ES>();
+  __shared__ uint32_t lds[DS_GROUP][MC_BLOCK / 64];
+  uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (walking the tiles from the end, so that the apply pass finds its first
+  // tiles among the ones read last, measured the same: 124-130 us either way
+  // for 256 MiB i1/i2/i4)
+  const size_t t0 = (size_t)blockIdx.x * DS_GROUP;
+  uint32_t acc[DS_GROUP];
+  if ((t0 + DS_GROUP) * TE <= n) {
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) {
+      const uint8_t *tb = src + (t0 + h) * TE * ES;
+      const mc_u32x4 w0 = mc_ld16<false>(tb + 16 * (size_t)threadIdx.x);
+      const mc_u32x4 w1 = mc_ld16<false>(tb + 16 * (size_t)(MC_BLOCK + threadIdx.x));
+      const uint32_t d[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      uint32_t a = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (ES == 1) a = __builtin_amdgcn_udot4(d[i], 0x01010101u, a, false);
+        else if constexpr (ES == 2) a = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d[i]), ushort2_t{1, 1}, a, false);
+        else a += d[i];
+      }
+      acc[h] = a;
+    }
+  } else {
+    constexpr int HALF = PER / 2;
+    dacc_t<ES> v[DS_GROUP][PER];
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) {
+      const size_t tb = (t0 + h) * TE;
+      ds_load_half<ES, false>(src, n, tb + (size_t)threadIdx.x * HALF, v[h], 0);
+      ds_load_half<ES, false>(src, n, tb + (size_t)(MC_BLOCK + threadIdx.x) * HALF, v[h], HALF);
+    }
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) {
+      acc[h] = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) acc[h] += (uint32_t)v[h][i];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) acc[h] += __shfl_xor(acc[h], off, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < DS_GROUP; ++h) lds[h][wave] = acc[h];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t tot = 0;
+  for (int h = 0; h < DS_GROUP; ++h) {
+    uint32_t a = 0;
+    for (int w = 0; w < MC_BLOCK / 64; ++w) a += lds[h][w];
+    if (t0 + h < ntiles) tile_tot[t0 + h] = a;
+    tot += a;
+  }
+  const size_t g = t0 / GT;
+  const size_t in_group = ntiles - g * GT < GT ? ntiles - g * GT : GT;
+  const unsigned long long arrivals = (in_group + DS_GROUP - 1) / DS_GROUP;
+  unsigned long long *word = reinterpret_cast<unsigned long long *>(ticket + (size_t)MC_ARRIVAL_LINE * g);
+  const unsigned long long old = atomicAdd(word, ((unsigned long long)tot << 16) | 1ull);
+  if ((old & 0xffffu) + 1u == arrivals) {
+    gtot[g] = (uint32_t)(old >> 16) + tot;
+    *word = 0;  // every arrival of this call is in: left zero
+  }
+}
+
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply_g(const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst, size_t n, const uint32_t *ws,
+                                                           size_t ntiles, unsigned GT) {
+  constexpr int PER = ds_per<ES>();
+  constexpr int H = PER / 2;
+  using T = dacc_t<ES>;  // uint32_t for ES <= 4
+  __shared__ T lds[3][MC_BLOCK / 64];
+  const uint32_t *tile_tot = ws, *gtot = ws + ntiles;
+  const size_t tile = blockIdx.x;
+  const size_t g = tile / GT, gt0 = g * GT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;  // before the data loads
+  for (unsigned j = threadIdx.x; j < GT && gt0 + j < tile; j += MC_BLOCK) x += tile_tot[gt0 + j];
+  const size_t ea0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * H;
+  const size_t eb0 = tile * ds_tile<ES>() + (size_t)(MC_BLOCK + threadIdx.x) * H;
+  T v[PER];
+  ds_load_half<ES, false>(src, n, ea0, v, 0);
+  ds_load_half<ES, false>(src, n, eb0, v, H);
+  T ra = 0, rb = 0;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    ra += v[i];
+    v[i] = ra;
+    rb += v[H + i];
+    v[H + i] = rb;
+  }
+  // one LDS round: the two-half exclusive scan and the block sum of x
+  T ia = ra, ib = rb;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T oa = __shfl_up(ia, off, 64), ob = __shfl_up(ib, off, 64);
+    if (lane >= off) {
+      ia += oa;
+      ib += ob;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  if (lane == 63) {
+    lds[0][wave] = ia;
+    lds[1][wave] = ib;
+  }
+  if (lane == 0) lds[2][wave] = x;
+  __syncthreads();
+  T pa = 0, pb = 0, ta = 0, pre = 0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) {
+    if (w < wave) {
+      pa += lds[0][w];
+      pb += lds[1][w];
+    }
+    ta += lds[0][w];
+    pre += lds[2][w];
+  }
+  const T ua = __shfl_up(ia, 1, 64), ub = __shfl_up(ib, 1, 64);
+  const T xa = pa + (lane ? ua : (T)0), xb = pb + (lane ? ub : (T)0);
+  const T qa = pre + xa, qb = pre + ta + xb;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    v[i] += qa;
+    v[H + i] += qb;
+  }
+  ds_store_half<ES>(dst, n, ea0, v, 0);
+  ds_store_half<ES>(dst, n, eb0, v, H);
+}
+
+template <int ES>
+static void launch_dscan_g(const uint8_t *s, uint8_t *d, size_t n, uint32_t *ws, uint32_t *ticket, hipStream_t st) {
+  const size_t ntiles = (n + ds_tile<ES>() - 1) / ds_tile<ES>();
+  const unsigned gt = ds_group_tiles(ntiles);
+  k_dscan_reduce_g<ES><<<(unsigned)((ntiles + DS_GROUP - 1) / DS_GROUP), MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles,
+                                                                                            gt);
+  k_dscan_apply_g<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
 }
 
 // MCODEC_DSCAN=0 selects the generic three-pass kernels (A/B)
@@ -1105,13 +1275,19 @@ extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
   if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n, dtype) : 0;
-  const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
-  const size_t fast = astype == dtype && dtype != MC_B1 ? dscan_ws_entries(n, mc_itemsize(dtype)) : 0;
-  return (generic > fast ? generic : fast) * sizeof(uint64_t);
+  const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE * sizeof(uint64_t);
+  if (astype != dtype || dtype == MC_B1) return generic;
+  const int es = mc_itemsize(dtype);
+  const size_t three_pass = dscan_ws_entries(n, es) * sizeof(uint64_t);
+  const size_t te = (size_t)(32 / es) * MC_BLOCK;
+  const size_t two_launch = ((n + te - 1) / te + DS_MAX_GROUPS) * sizeof(uint32_t);  // tile + group totals
+  size_t w = generic > three_pass ? generic : three_pass;
+  return w > two_launch ? w : two_launch;
 }
 
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
-                    size_t workspace_bytes, mc_stream_t stream) {
+                    size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
+  if (ticket && (uintptr_t)ticket % 8) return MC_EINVAL;
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
   if (n == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;
@@ -1137,6 +1313,16 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
   uint64_t *sums = static_cast<uint64_t *>(workspace);
   if (astype == dtype && dtype != MC_B1 && ((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0 &&
       dscan_enabled()) {
+    const int es = mc_itemsize(dtype);
+    // two launches with a ticket while groups stay <= 1024 tiles (the apply
+    // workgroup sums its group's earlier tile totals, 4 per thread)
+    if (ticket && es <= 4 && ds_group_tiles((n + (size_t)(32 / es) * MC_BLOCK - 1) / ((size_t)(32 / es) * MC_BLOCK)) <= 1024) {
+      uint32_t *ws = static_cast<uint32_t *>(workspace);
+      if (es == 1) launch_dscan_g<1>(s, d, n, ws, ticket, st);
+      else if (es == 2) launch_dscan_g<2>(s, d, n, ws, ticket, st);
+      else launch_dscan_g<4>(s, d, n, ws, ticket, st);
+      return mc_last_launch();
+    }
     switch (mc_itemsize(dtype)) {
       case 1: launch_dscan<1>(s, d, n, sums, st); break;
       case 2: launch_dscan<2>(s, d, n, sums, st); break;

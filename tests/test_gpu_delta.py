@@ -185,3 +185,32 @@ def test_delta_encode_first_element_assignment(device, dt, astype, first):
             batch.delta_chunks(torch.from_numpy(np.stack([x[[1, 2, 0]], x])).to(device), Delta(dt, astype))
         return
     assert Delta(dt, astype).encode(torch.from_numpy(x).to(device)).cpu().numpy().tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("dt,n", [("|i1", 8192 * 300 + 5), ("|u1", 8192 * 16384 + 8192 * 7 + 3), ("<i2", 4096 * 513),
+                                  ("<u2", 4096 * 777 + 1), ("<i4", 2048 * 70000 + 9), ("<u4", 17)])
+def test_two_launch_int_decode_vs_oracle(device, dt, n):
+    """Same-width integer Delta decode, default path (two launches: group
+    totals by one 64-bit arrival atomic per 4-tile workgroup, prefixes in the
+    apply pass) against the oracle and against the three-pass scan (the ABI
+    with no ticket); one group and many, ragged tails, groups of 512 tiles;
+    the stream's ticket is left zero."""
+    from numcodecs_amd import _native, _ops
+
+    rng = np.random.default_rng(n)
+    info = np.iinfo(np.dtype(dt))
+    enc = rng.integers(info.min, info.max, n, endpoint=True, dtype=np.dtype(dt))
+    src = torch.from_numpy(enc).to(device)
+    d = Delta(dtype=dt)
+    dec = d.decode(src)
+    ref = oracle.delta_decode(enc, dt)
+    assert np.array_equal(dec.cpu().numpy().view(np.dtype(dt)), ref)
+    a = _ops.dtype_code(dt)
+    ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=device)
+    out = torch.empty_like(src)
+    _native.check(_native.lib.mc_delta_decode(src.data_ptr(), out.data_ptr(), n, a, a, ws.data_ptr(), ws_n, None,
+                                              _ops.stream(src)), "three-pass")
+    assert torch.equal(out.view(torch.uint8), dec.reshape(-1).view(torch.uint8))
+    torch.cuda.synchronize()
+    assert not _ops._verify_slot(src, _ops.stream(src)).ticket.any()

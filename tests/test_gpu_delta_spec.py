@@ -61,7 +61,7 @@ def _decode_raw(enc_np, dt):
     assert ws_n == (2 * ntiles + 1) * 8
     ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
     _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
-                                              _ops.stream(src)), "mc_delta_decode")
+                                              None, _ops.stream(src)), "mc_delta_decode")
     torch.cuda.synchronize()
     return dst.cpu().numpy(), int(ws[-1].item())
 
@@ -156,7 +156,7 @@ def test_repeated_calls_reset_failure_word(device, dt):
         src = torch.from_numpy(enc).to(dev)
         dst = torch.empty_like(src)
         _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
-                                                  _ops.stream(src)), "mc_delta_decode")
+                                                  None, _ops.stream(src)), "mc_delta_decode")
         assert dst.cpu().numpy().tobytes() == _oracle_dec(enc, dt).tobytes()
         assert int(ws[-1].item()) == (n if enc is good else 7)
 
