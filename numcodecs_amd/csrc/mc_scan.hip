@@ -163,13 +163,19 @@ MC_DEV void ser_st(T *p, const T (&r)[SER_G]) {
 
 constexpr int SER_UN = 8;              // vectors of 4 elements in flight per lane
 
-template <int A_, int D, bool VEC, int SER_SLOT_BYTES = 32768, int SER_G = 16>
+// L: numpy's loop dtype for cumsum(enc: A, out=dec: D) is
+// np.promote_types(A, D) (mc_float_loop_dtype): the running sum is kept in L
+// and each result is cast to D on output (f8 input into f4 output
+// accumulates in f8; f2 output of f4 input accumulates in f4).  The fix-up
+// mode (startp) reads its carry back from dst, so it needs L == D.
+template <int A_, int D, bool VEC, int SER_SLOT_BYTES = 32768, int SER_G = 16, int L = D>
 __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__ src,
                                                      size_t src_stride,
                                                      uint8_t *__restrict__ dst,
                                                      size_t dst_stride, size_t n, int a_rt,
                                                      const uint64_t *__restrict__ startp = nullptr) {
-  using T = typename SerAcc<D>::T;
+  static_assert(L == D || L == MC_F4 || L == MC_F8, "loop dtype");
+  using T = typename SerAcc<L>::T;
   constexpr int BLK = SER_SLOT_BYTES / (int)sizeof(T);
   constexpr int DS = D == MC_F8 ? 8 : (D == MC_F4 ? 4 : 2);
   __shared__ __attribute__((aligned(16))) T slot[2][BLK + 2 * SER_G];
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
   // verified value before it; nothing to do if every element verified
   bool has_carry = false;
   T carry = 0;
-  if (startp) {
+  if (L == D && startp) {
     size_t s0 = (size_t)startp[blockIdx.x];
     if (s0 >= n) return;
     // restart on a 128-B line of dst: the chain's block loads/stores stay
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
   const size_t nb = (n + BLK - 1) / BLK;
 
   auto to_acc = [&](uint64_t bits) -> T {
-    return (T)mc_num_cast(mc_num_from_bits(bits, a), a, D).f;
+    return (T)mc_num_cast(mc_num_from_bits(bits, a), a, L).f;
   };
   auto load_blk = [&](size_t b) {  // wave 1: src block b -> slot[b & 1]
     const size_t b0 = b * BLK;
@@ -241,7 +247,9 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
       uint64_t o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        o[k] = j + k < cnt ? mc_num_to_bits(mc_num_f((double)p[j + k]), D) : 0;
+        o[k] = j + k < cnt ? (L == D ? mc_num_to_bits(mc_num_f((double)p[j + k]), D)
+                                     : mc_num_to_bits(mc_num_cast(mc_num_f((double)p[j + k]), L, D), D))
+                           : 0;
       if (VEC && j + 4 <= cnt) {
         mc_store4(dst + (b0 + j) * DS, DS, o);
       } else {
@@ -264,11 +272,11 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
       const int cnt = (int)min((size_t)BLK, n - b * BLK);
       int j = 0;
       if (b == 0) {  // out[0] = x[0] exactly (no add), then align to a group
-        acc = has_carry ? ser_add<D>(carry, p[0]) : p[0];
+        acc = has_carry ? ser_add<L>(carry, p[0]) : p[0];
         p[0] = acc;
         const int m = cnt < SER_G ? cnt : SER_G;
         for (int k = 1; k < m; ++k) {
-          acc = ser_add<D>(acc, p[k]);
+          acc = ser_add<L>(acc, p[k]);
           p[k] = acc;
         }
         j = m;
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
           __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead ahead of the adds
 #pragma unroll
           for (int k = 0; k < SER_G; ++k) {
-            acc = ser_add<D>(acc, ga[k]);
+            acc = ser_add<L>(acc, ga[k]);
             ga[k] = acc;
           }
           ser_st<T, SER_G>(p + j, ga);
@@ -292,14 +300,14 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int k = 0; k < SER_G; ++k) {
-            acc = ser_add<D>(acc, gb[k]);
+            acc = ser_add<L>(acc, gb[k]);
             gb[k] = acc;
           }
           ser_st<T, SER_G>(p + j + SER_G, gb);
         }
       }
       for (; j < cnt; ++j) {
-        acc = ser_add<D>(acc, p[j]);
+        acc = ser_add<L>(acc, p[j]);
         p[j] = acc;
       }
     }
@@ -311,10 +319,42 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
 // (slot bytes, group) per schedule: a 32 KiB slot amortises the block
 // barrier for one long chain; a batch needs small slots so that many chains
 // (workgroups) fit a CU's LDS at once (2 x 32 KiB slots allow only 2).
+// numpy's loop dtype of cumsum(enc: a, out=dec: d) for a float d:
+// np.promote_types(a, d) (pinned against numpy for every pair by
+// tests/test_gpu_delta_spec2.py): the wider float; an integer promotes to the
+// smallest float that holds it (1-byte -> f2, 2-byte -> f4, wider -> f8)
+static int mc_float_loop_dtype(int a, int d) {
+  auto rank = [](int t) { return t == MC_F8 ? 3 : t == MC_F4 ? 2 : t == MC_F2 ? 1 : 0; };
+  int fa;
+  if (mc_is_float(a)) fa = a;
+  else if (a == MC_B1 || mc_itemsize(a) == 1) fa = MC_F2;
+  else if (mc_itemsize(a) == 2) fa = MC_F4;
+  else fa = MC_F8;
+  return rank(fa) > rank(d) ? fa : d;
+}
+
 template <int D>
 static void launch_serial(const uint8_t *s, size_t ss, uint8_t *d, size_t dss, size_t n,
                           size_t rows, int a, hipStream_t st, int variant = 0) {
   const int as = mc_itemsize(a);
+  const int loop = mc_float_loop_dtype(a, D);
+  if (loop != D) {  // accumulate in the wider loop dtype, cast each result to D
+    const bool v = ((uintptr_t)s % (4 * as) == 0) && (ss % (4 * as) == 0) &&
+                   ((uintptr_t)d % (4 * mc_itemsize(D)) == 0) && (dss % (4 * mc_itemsize(D)) == 0);
+    const unsigned g = (unsigned)rows;
+    if constexpr (D != MC_F8) {
+      if (loop == MC_F8) {
+        if (v) k_scan_serial<-1, D, true, 8192, 16, MC_F8><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+        else k_scan_serial<-1, D, false, 8192, 16, MC_F8><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+        return;
+      }
+    }
+    if constexpr (D == MC_F2) {
+      if (v) k_scan_serial<-1, D, true, 8192, 16, MC_F4><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+      else k_scan_serial<-1, D, false, 8192, 16, MC_F4><<<g, 128, 0, st>>>(s, ss, d, dss, n, a);
+    }
+    return;
+  }
   const bool vec = ((uintptr_t)s % (4 * as) == 0) && (ss % (4 * as) == 0) &&
                    ((uintptr_t)d % (4 * mc_itemsize(D)) == 0) && (dss % (4 * mc_itemsize(D)) == 0);
   // measured (tools/probe_delta.py, profiles/r01/probe_delta.json): one chain
@@ -920,33 +960,119 @@ static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, h
 // serial again.  The output is bit-exact for any input; the data only decide
 // how much of the chunk runs at scan speed instead of one add per element.
 // ---------------------------------------------------------------------------
-// A thread holds FS_Q 16-B vectors (FS_W elements each) in FS_Q segments of
-// the tile: segment q is 16*MC_BLOCK contiguous bytes and thread t owns its
-// vector at 16*t, so every wave load/store covers 1 KiB contiguously; 16 KiB
-// per tile (4096 f4 / 2048 f8 elements).
-template <typename T> constexpr int fs_w() { return 16 / (int)sizeof(T); }
-constexpr int FS_Q = 4;
-template <typename T> constexpr size_t fs_tile() { return (size_t)fs_w<T>() * FS_Q * MC_BLOCK; }
+// A thread holds FS_Q 16-B vectors of OUTPUT elements (W = 16 / itemsize(D)
+// each) in FS_Q segments of the tile: segment q is W*MC_BLOCK contiguous
+// elements and thread t owns its vector at W*t, so every wave store covers
+// 1 KiB contiguously; 16 KiB of output per tile (8192 f2 / 4096 f4 / 2048 f8
+// elements).
+//
+// FsT<A_, D> is the element model, numpy's cumsum(enc, out=dec) with enc of
+// dtype A (astype) and dec of dtype D (a float dtype), exactly as the serial
+// chain runs it (k_scan_serial): every input is first cast to D
+// (mc_num_cast), the adds happen in D -- f2 as float32 adds rounded to half
+// per step (ser_add<MC_F2>) -- and c_0 = D(enc_0).  A_ = D loads 16-B
+// vectors of D; A_ = -1 (any other astype, given at run time) loads element
+// by element and casts.  The double-precision scan only proposes candidates;
+// the per-element check against that recurrence decides, so the candidate
+// rounding (double -> D) need not match numpy's.
+template <int D> struct FsStore { using S = float; using V = float; };
+template <> struct FsStore<MC_F8> { using S = double; using V = double; };
+template <> struct FsStore<MC_F2> { using S = _Float16; using V = float; };
 
-template <typename T>
+template <int A_, int D>
+struct FsT {
+  using S = typename FsStore<D>::S;  // stored element
+  using V = typename FsStore<D>::V;  // arithmetic value (numpy's loop type)
+  static constexpr int W = 16 / (int)sizeof(S);
+  typedef S svec __attribute__((ext_vector_type(W)));
+  MC_DEV static V from_bits(uint64_t bits, int a) {  // enc element -> its D value
+    return (V)mc_num_cast(mc_num_from_bits(bits, a), a, D).f;
+  }
+  MC_DEV static S round(double x) { return (S)x; }  // candidate (any rounding)
+  MC_DEV static V val(S c) { return (V)c; }
+  MC_DEV static S store(V r) { return (S)r; }  // exact: r holds a D value
+  MC_DEV static V step(V pv, V x) { return ser_add<D>(pv, x); }
+  MC_DEV static uint64_t bits(S c) {
+    if constexpr (sizeof(S) == 8) return __builtin_bit_cast(uint64_t, c);
+    else if constexpr (sizeof(S) == 4) return __builtin_bit_cast(uint32_t, c);
+    else return __builtin_bit_cast(uint16_t, c);
+  }
+  MC_DEV static bool finite(S c) {
+    if constexpr (sizeof(S) == 8) return __builtin_isfinite(c);
+    else return __builtin_isfinite((float)c);
+  }
+  // the candidate of lane - 1 (bit pattern moved through an integer shuffle)
+  MC_DEV static S shfl_up1(S c) {
+    if constexpr (sizeof(S) == 8) {
+      return __builtin_bit_cast(S, (unsigned long long)__shfl_up(__builtin_bit_cast(unsigned long long, c), 1, 64));
+    } else if constexpr (sizeof(S) == 4) {
+      return __builtin_bit_cast(S, (unsigned int)__shfl_up(__builtin_bit_cast(unsigned int, c), 1, 64));
+    } else {
+      const unsigned int b = __shfl_up((unsigned int)__builtin_bit_cast(uint16_t, c), 1, 64);
+      return __builtin_bit_cast(S, (uint16_t)b);
+    }
+  }
+};
+
+constexpr int FS_Q = 4;
+MC_HD constexpr int fs_w_of(int d) { return d == MC_F8 ? 2 : (d == MC_F4 ? 4 : 8); }
+MC_HD constexpr size_t fs_tile_of(int d) { return (size_t)fs_w_of(d) * FS_Q * MC_BLOCK; }
+template <int D> constexpr size_t fs_tile() { return fs_tile_of(D); }
+
+template <int D>
 MC_DEV size_t fs_elem0(size_t t0, int q) {  // first element of this thread's vector in segment q
-  return t0 + (size_t)q * fs_w<T>() * MC_BLOCK + (size_t)threadIdx.x * fs_w<T>();
+  return t0 + (size_t)q * fs_w_of(D) * MC_BLOCK + (size_t)threadIdx.x * fs_w_of(D);
 }
 
-template <typename T>
-MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, T (&v)[FS_Q][fs_w<T>()]) {
-  typedef T vec __attribute__((ext_vector_type(fs_w<T>())));
-  constexpr int W = fs_w<T>();
+template <int A_, int D>
+MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, int a,
+                    typename FsT<A_, D>::V (&v)[FS_Q][FsT<A_, D>::W]) {
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
+  if constexpr (A_ == D) {
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const size_t e0 = fs_elem0<D>(t0, q);
+      if (e0 + W <= n) {
+        const typename Tr::svec x =
+            __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
+#pragma unroll
+        for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e)
+          v[q][e] = e0 + e < n ? (typename Tr::V)reinterpret_cast<const typename Tr::S *>(src)[e0 + e]
+                               : (typename Tr::V)0;
+      }
+    }
+  } else {
+    const int as = mc_itemsize(a);
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const size_t e0 = fs_elem0<D>(t0, q);
+      uint64_t b[W];
+#pragma unroll
+      for (int e = 0; e < W; ++e) b[e] = e0 + e < n ? mc_load_elem_u(src, e0 + e, as) : 0;
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = e0 + e < n ? Tr::from_bits(b[e], a) : (typename Tr::V)0;
+    }
+  }
+}
+
+template <int A_, int D>
+MC_DEV void fs_store(uint8_t *dst, size_t n, size_t t0, const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W]) {
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
-    const size_t e0 = fs_elem0<T>(t0, q);
+    const size_t e0 = fs_elem0<D>(t0, q);
     if (e0 + W <= n) {
-      const vec x = __builtin_nontemporal_load(reinterpret_cast<const vec *>(src + e0 * sizeof(T)));
+      typename Tr::svec x;
 #pragma unroll
-      for (int e = 0; e < W; ++e) v[q][e] = x[e];
+      for (int e = 0; e < W; ++e) x[e] = c[q][e];
+      __builtin_nontemporal_store(x, reinterpret_cast<typename Tr::svec *>(dst + e0 * sizeof(typename Tr::S)));
     } else {
-#pragma unroll
-      for (int e = 0; e < W; ++e) v[q][e] = e0 + e < n ? reinterpret_cast<const T *>(src)[e0 + e] : (T)0;
+      for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<typename Tr::S *>(dst)[e0 + e] = c[q][e];
     }
   }
 }
@@ -954,10 +1080,8 @@ MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, T (&v)[FS_Q][fs_w<T
 // p[q][e] = the tile-relative inclusive prefix sum (double) of this thread's
 // element e of segment q.  Fixed association (element, lane, wave, segment
 // order), so the reduce and apply passes compute bitwise the same values.
-template <typename T>
-MC_DEV void fs_tile_scan(const T (&v)[FS_Q][fs_w<T>()], double (&p)[FS_Q][fs_w<T>()],
-                         double (&lds)[FS_Q][MC_BLOCK / 64]) {
-  constexpr int W = fs_w<T>();
+template <typename V, int W>
+MC_DEV void fs_tile_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double (&lds)[FS_Q][MC_BLOCK / 64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double incl[FS_Q];
 #pragma unroll
@@ -998,37 +1122,60 @@ MC_DEV void fs_tile_scan(const T (&v)[FS_Q][fs_w<T>()], double (&p)[FS_Q][fs_w<T
   }
 }
 
-template <typename T>
-MC_DEV uint64_t fs_bits(T x) {
-  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(uint64_t, x);
-  else return __builtin_bit_cast(uint32_t, x);
+// The smallest global index in this thread's FS_Q x W candidates c whose
+// value differs (bitwise) from numpy's recurrence D(pred + x), or that is
+// not finite; ~0 if none.  p0[q] = the predecessor candidate of the
+// thread's first element of segment q.
+template <int A_, int D>
+MC_DEV uint64_t fs_check(const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W],
+                         const typename FsT<A_, D>::V (&v)[FS_Q][FsT<A_, D>::W],
+                         const typename FsT<A_, D>::S (&p0)[FS_Q], size_t t0, size_t n) {
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
+  uint64_t first = ~(uint64_t)0;
+#pragma unroll
+  for (int q = FS_Q - 1; q >= 0; --q) {  // descending: the last hit is the smallest index
+    const size_t e0 = fs_elem0<D>(t0, q);
+#pragma unroll
+    for (int e = W - 1; e >= 0; --e) {
+      const size_t g = e0 + e;
+      const typename Tr::S pv = e ? c[q][e - 1] : p0[q];
+      const typename Tr::S r = g == 0 ? Tr::store(v[q][0]) : Tr::store(Tr::step(Tr::val(pv), v[q][e]));
+      // a non-finite input makes its own prefix (and so c) non-finite
+      const bool ok = Tr::bits(c[q][e]) == Tr::bits(r) && Tr::finite(c[q][e]);
+      if (g < n && !ok) first = g;
+    }
+  }
+  return first;
 }
 
-template <typename T>
-__global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n,
+template <int A_, int D>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n, int a,
                                                           double *__restrict__ sums) {
-  constexpr int W = fs_w<T>();
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
   __shared__ double lds[FS_Q][MC_BLOCK / 64];
-  T v[FS_Q][W];
-  fs_load<T>(src, n, (size_t)blockIdx.x * fs_tile<T>(), v);
+  typename Tr::V v[FS_Q][W];
+  fs_load<A_, D>(src, n, (size_t)blockIdx.x * fs_tile<D>(), a, v);
   double p[FS_Q][W];
-  fs_tile_scan<T>(v, p, lds);
+  fs_tile_scan<typename Tr::V, W>(v, p, lds);
   if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = p[FS_Q - 1][W - 1];
 }
 
-template <typename T>
+template <int A_, int D>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restrict__ src,
-                                                         uint8_t *__restrict__ dst, size_t n,
+                                                         uint8_t *__restrict__ dst, size_t n, int a,
                                                          const double *__restrict__ sums,
                                                          const double *__restrict__ pre_t,
                                                          uint64_t *__restrict__ fail) {
-  constexpr int W = fs_w<T>();
-  typedef T vec __attribute__((ext_vector_type(W)));
+  using Tr = FsT<A_, D>;
+  using S = typename Tr::S;
+  constexpr int W = Tr::W;
   __shared__ double lds[FS_Q][MC_BLOCK / 64];
-  __shared__ T ldsc[FS_Q][MC_BLOCK / 64];
+  __shared__ S ldsc[FS_Q][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t tile = blockIdx.x;
-  const size_t t0 = tile * fs_tile<T>();
+  const size_t t0 = tile * fs_tile<D>();
   // a tile at or past a recorded failure is recomputed by the serial fix-up.
   // Each wave reads the word itself, so waves of one workgroup may disagree
   // when another tile's atomicMin lands in between: the exited waves leave
@@ -1037,53 +1184,32 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   // whole tile lies at or past a recorded failure, so the fix-up rewrites
   // it, and any index these waves report is >= t0, above the minimum.
   if (__builtin_nontemporal_load(fail) <= t0) return;
-  T v[FS_Q][W];
-  fs_load<T>(src, n, t0, v);
+  typename Tr::V v[FS_Q][W];
+  fs_load<A_, D>(src, n, t0, a, v);
   double p[FS_Q][W];
-  fs_tile_scan<T>(v, p, lds);
-  const double S = pre_t[tile];  // the tile's prefix
-  T c[FS_Q][W], up[FS_Q];
+  fs_tile_scan<typename Tr::V, W>(v, p, lds);
+  const double Sp = pre_t[tile];  // the tile's prefix
+  S c[FS_Q][W], up[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
 #pragma unroll
-    for (int e = 0; e < W; ++e) c[q][e] = (T)(S + p[q][e]);
-    up[q] = __shfl_up(c[q][W - 1], 1, 64);
+    for (int e = 0; e < W; ++e) c[q][e] = Tr::round(Sp + p[q][e]);
+    up[q] = Tr::shfl_up1(c[q][W - 1]);
     if (lane == 63) ldsc[q][wave] = c[q][W - 1];
   }
   __syncthreads();
   // the tile's last candidate in the previous tile: the same double sum it
   // was rounded from there (sums[] is that tile's last prefix, bitwise)
-  const T pbound = tile ? (T)(pre_t[tile - 1] + sums[tile - 1]) : (T)0;
-  uint64_t first = ~(uint64_t)0;
-#pragma unroll
-  for (int q = FS_Q - 1; q >= 0; --q) {  // descending: the last hit is the smallest index
-    T p0;
-    if (lane) p0 = up[q];
-    else if (wave) p0 = ldsc[q][wave - 1];
-    else p0 = q ? ldsc[q - 1][MC_BLOCK / 64 - 1] : pbound;
-    const size_t e0 = fs_elem0<T>(t0, q);
-#pragma unroll
-    for (int e = W - 1; e >= 0; --e) {
-      const size_t g = e0 + e;
-      const T pv = e ? c[q][e - 1] : p0;
-      const T r = g == 0 ? v[q][0] : (T)(pv + v[q][e]);
-      // a non-finite input makes its own prefix (and so c) non-finite
-      const bool ok = fs_bits<T>(c[q][e]) == fs_bits<T>(r) && __builtin_isfinite(c[q][e]);
-      if (g < n && !ok) first = g;
-    }
-  }
+  const S pbound = tile ? Tr::round(pre_t[tile - 1] + sums[tile - 1]) : (S)0;
+  S p0[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
-    const size_t e0 = fs_elem0<T>(t0, q);
-    if (e0 + W <= n) {
-      vec x;
-#pragma unroll
-      for (int e = 0; e < W; ++e) x[e] = c[q][e];
-      __builtin_nontemporal_store(x, reinterpret_cast<vec *>(dst + e0 * sizeof(T)));
-    } else {
-      for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<T *>(dst)[e0 + e] = c[q][e];
-    }
+    if (lane) p0[q] = up[q];
+    else if (wave) p0[q] = ldsc[q][wave - 1];
+    else p0[q] = q ? ldsc[q - 1][MC_BLOCK / 64 - 1] : pbound;
   }
+  uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
+  fs_store<A_, D>(dst, n, t0, c);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const uint64_t o = __shfl_xor(first, off, 64);
@@ -1100,60 +1226,52 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
 // records the tile's start in fail[row] and stops without storing it;
 // k_scan_serial (fix-up mode, one chain per row) then finishes that row.
 // fail[row] = n when the whole row verified.
-template <typename T>
+template <int A_, int D>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restrict__ src,
                                                         size_t src_stride, uint8_t *__restrict__ dst,
-                                                        size_t dst_stride, size_t n,
+                                                        size_t dst_stride, size_t n, int a,
                                                         uint64_t *__restrict__ fail) {
-  constexpr int W = fs_w<T>();
-  typedef T vec __attribute__((ext_vector_type(W)));
+  using Tr = FsT<A_, D>;
+  using S = typename Tr::S;
+  constexpr int W = Tr::W;
   __shared__ double lds[2][FS_Q][MC_BLOCK / 64];
-  __shared__ T ldsc[2][FS_Q][MC_BLOCK / 64];
+  __shared__ S ldsc[2][FS_Q][MC_BLOCK / 64];
   __shared__ uint64_t ldsf[2][MC_BLOCK / 64];
   __shared__ double ldsp[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
   double carry = 0.0;
-  T prevc = (T)0;
+  S prevc = (S)0;
   int par = 0;
-  T nv[FS_Q][W];
-  fs_load<T>(src, n, 0, nv);
-  for (size_t t0 = 0; t0 < n; t0 += fs_tile<T>(), par ^= 1) {
-    T v[FS_Q][W];
+  typename Tr::V nv[FS_Q][W];
+  fs_load<A_, D>(src, n, 0, a, nv);
+  for (size_t t0 = 0; t0 < n; t0 += fs_tile<D>(), par ^= 1) {
+    typename Tr::V v[FS_Q][W];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
       for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
-    if (t0 + fs_tile<T>() < n) fs_load<T>(src, n, t0 + fs_tile<T>(), nv);  // next tile in flight
+    if (t0 + fs_tile<D>() < n) fs_load<A_, D>(src, n, t0 + fs_tile<D>(), a, nv);  // next tile in flight
     double p[FS_Q][W];
-    fs_tile_scan<T>(v, p, lds[par]);
-    T c[FS_Q][W], up[FS_Q];
+    fs_tile_scan<typename Tr::V, W>(v, p, lds[par]);
+    S c[FS_Q][W], up[FS_Q];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q) {
 #pragma unroll
-      for (int e = 0; e < W; ++e) c[q][e] = (T)(carry + p[q][e]);
-      up[q] = __shfl_up(c[q][W - 1], 1, 64);
+      for (int e = 0; e < W; ++e) c[q][e] = Tr::round(carry + p[q][e]);
+      up[q] = Tr::shfl_up1(c[q][W - 1]);
       if (lane == 63) ldsc[par][q][wave] = c[q][W - 1];
     }
     __syncthreads();
-    uint64_t first = ~(uint64_t)0;
+    S p0[FS_Q];
 #pragma unroll
-    for (int q = FS_Q - 1; q >= 0; --q) {
-      T p0;
-      if (lane) p0 = up[q];
-      else if (wave) p0 = ldsc[par][q][wave - 1];
-      else p0 = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
-      const size_t e0 = fs_elem0<T>(t0, q);
-#pragma unroll
-      for (int e = W - 1; e >= 0; --e) {
-        const size_t g = e0 + e;
-        const T pv = e ? c[q][e - 1] : p0;
-        const T r = g == 0 ? v[q][0] : (T)(pv + v[q][e]);
-        const bool ok = fs_bits<T>(c[q][e]) == fs_bits<T>(r) && __builtin_isfinite(c[q][e]);
-        if (g < n && !ok) first = g;
-      }
+    for (int q = 0; q < FS_Q; ++q) {
+      if (lane) p0[q] = up[q];
+      else if (wave) p0[q] = ldsc[par][q][wave - 1];
+      else p0[q] = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
     }
+    uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const uint64_t o = __shfl_xor(first, off, 64);
@@ -1172,18 +1290,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
       if (threadIdx.x == 0) fail[blockIdx.x] = t0;
       return;
     }
-#pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
-      const size_t e0 = fs_elem0<T>(t0, q);
-      if (e0 + W <= n) {
-        vec x;
-#pragma unroll
-        for (int e = 0; e < W; ++e) x[e] = c[q][e];
-        __builtin_nontemporal_store(x, reinterpret_cast<vec *>(dst + e0 * sizeof(T)));
-      } else {
-        for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<T *>(dst)[e0 + e] = c[q][e];
-      }
-    }
+    fs_store<A_, D>(dst, n, t0, c);
     // next tile: prefix = this tile's last prefix (thread MC_BLOCK-1's, via
     // LDS), predecessor = this tile's last candidate
     carry = ldsp[par];
@@ -1202,8 +1309,17 @@ static bool fspec_enabled() {
 }
 
 static size_t fspec_ntiles(size_t n, int dt) {
-  const size_t te = dt == MC_F8 ? fs_tile<double>() : fs_tile<float>();
+  const size_t te = fs_tile_of(dt);
   return (n + te - 1) / te;
+}
+
+// the speculative decode serves any float dtype D with any numeric astype
+// except bool whose loop dtype is D (casts as numpy's cumsum(enc, out=dec)
+// does); a wider loop dtype (f8 astype into f4, ...) runs the serial chain
+static bool fspec_types_ok(int astype, int dtype) {
+  // the fix-up restarts from dtype values, so the loop dtype must be dtype
+  return mc_is_float(dtype) && mc_valid_dtype(astype) && astype != MC_B1 &&
+         mc_float_loop_dtype(astype, dtype) == dtype;
 }
 
 // tile totals, tile prefixes, the failure word
@@ -1253,16 +1369,54 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict
   if (blockIdx.x == 0 && threadIdx.x == 0) *fail = n;
 }
 
-template <int D>
-static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, void *ws, hipStream_t st) {
-  using T = typename std::conditional<D == MC_F8, double, float>::type;
+template <int A_, int D>
+static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st) {
   const size_t ntiles = fspec_ntiles(n, D);
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
   uint64_t *fail = reinterpret_cast<uint64_t *>(pre + ntiles);
-  k_fspec_reduce<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, sums);
+  k_fspec_reduce<A_, D><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
   k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, fail, n);
-  k_fspec_apply<T><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, sums, pre, fail);
-  k_scan_serial<D, D, true, 32768, 32><<<1, 128, 0, st>>>(s, 0, d, 0, n, D, fail);
+  k_fspec_apply<A_, D><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, pre, fail);
+  k_scan_serial<A_, D, true, 32768, 32><<<1, 128, 0, st>>>(s, 0, d, 0, n, a, fail);
+}
+
+static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int dt, void *ws, hipStream_t st) {
+  if (dt == MC_F8) {
+    if (a == MC_F8) launch_fspec<MC_F8, MC_F8>(s, d, n, a, ws, st);
+    else launch_fspec<-1, MC_F8>(s, d, n, a, ws, st);
+  } else if (dt == MC_F4) {
+    if (a == MC_F4) launch_fspec<MC_F4, MC_F4>(s, d, n, a, ws, st);
+    else launch_fspec<-1, MC_F4>(s, d, n, a, ws, st);
+  } else {
+    if (a == MC_F2) launch_fspec<MC_F2, MC_F2>(s, d, n, a, ws, st);
+    else launch_fspec<-1, MC_F2>(s, d, n, a, ws, st);
+  }
+}
+
+// rows that failed verification finish as one serial chain each (the
+// schedules of launch_serial: small LDS slots when many chains share a CU;
+// 4 KiB slots measured no different here)
+template <int A_, int D>
+static void launch_fspec_rows(const uint8_t *sc, size_t src_stride, uint8_t *dc, size_t dst_stride, size_t n, int a,
+                              uint64_t *fail, unsigned g, hipStream_t st) {
+  k_fspec_rows<A_, D><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
+  constexpr int GRP = D == MC_F8 ? 16 : 32;
+  if (g >= 256) k_scan_serial<A_, D, true, 8192, GRP><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
+  else k_scan_serial<A_, D, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
+}
+
+static void launch_fspec_rows_any(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a, int dt,
+                                  uint64_t *fail, unsigned g, hipStream_t st) {
+  if (dt == MC_F8) {
+    if (a == MC_F8) launch_fspec_rows<MC_F8, MC_F8>(sc, ss, dc, ds, n, a, fail, g, st);
+    else launch_fspec_rows<-1, MC_F8>(sc, ss, dc, ds, n, a, fail, g, st);
+  } else if (dt == MC_F4) {
+    if (a == MC_F4) launch_fspec_rows<MC_F4, MC_F4>(sc, ss, dc, ds, n, a, fail, g, st);
+    else launch_fspec_rows<-1, MC_F4>(sc, ss, dc, ds, n, a, fail, g, st);
+  } else {
+    if (a == MC_F2) launch_fspec_rows<MC_F2, MC_F2>(sc, ss, dc, ds, n, a, fail, g, st);
+    else launch_fspec_rows<-1, MC_F2>(sc, ss, dc, ds, n, a, fail, g, st);
+  }
 }
 
 }  // namespace
@@ -1274,7 +1428,7 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
-  if (mc_is_float(dtype)) return astype == dtype && dtype != MC_F2 ? fspec_ws_bytes(n, dtype) : 0;
+  if (mc_is_float(dtype)) return fspec_types_ok(astype, dtype) ? fspec_ws_bytes(n, dtype) : 0;
   const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE * sizeof(uint64_t);
   if (astype != dtype || dtype == MC_B1) return generic;
   const int es = mc_itemsize(dtype);
@@ -1298,11 +1452,10 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
     // speculative parallel scan + verification, serial fix-up (above); the
     // plain serial chain where the preconditions (workspace, alignment,
     // astype == dtype, f4/f8) do not hold
-    if (astype == dtype && dtype != MC_F2 && fspec_enabled() && workspace &&
+    if (fspec_types_ok(astype, dtype) && fspec_enabled() && workspace &&
         workspace_bytes >= fspec_ws_bytes(n, dtype) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
         (uintptr_t)workspace % 8 == 0) {
-      if (dtype == MC_F8) launch_fspec<MC_F8>(s, d, n, workspace, st);
-      else launch_fspec<MC_F4>(s, d, n, workspace, st);
+      launch_fspec_any(s, d, n, astype, dtype, workspace, st);
       return mc_last_launch();
     }
     launch_serial_any(s, 0, d, 0, n, 1, astype, dtype, st);
@@ -1356,13 +1509,13 @@ int mc_delta_decode_batch(const void *src, size_t src_stride, void *dst, size_t 
 
 size_t mc_delta_decode_batch_workspace(size_t nchunks, size_t n, int astype, int dtype) {
   (void)n;
-  return astype == dtype && (dtype == MC_F4 || dtype == MC_F8) ? nchunks * sizeof(uint64_t) : 0;
+  return fspec_types_ok(astype, dtype) ? nchunks * sizeof(uint64_t) : 0;
 }
 
 int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst, size_t dst_stride,
                              size_t nchunks, size_t n, int astype, int dtype, void *workspace,
                              size_t workspace_bytes, mc_stream_t stream) {
-  const bool spec = astype == dtype && (dtype == MC_F4 || dtype == MC_F8) && fspec_enabled() && workspace &&
+  const bool spec = fspec_types_ok(astype, dtype) && fspec_enabled() && workspace &&
                     workspace_bytes >= nchunks * sizeof(uint64_t) && (uintptr_t)workspace % 8 == 0 &&
                     (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
                     (nchunks == 1 || (src_stride % 16 == 0 && dst_stride % 16 == 0));
@@ -1378,18 +1531,7 @@ int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst, size
     const unsigned g = (unsigned)min(GRID_MAX, nchunks - c0);
     const uint8_t *sc = s + c0 * src_stride;
     uint8_t *dc = d + c0 * dst_stride;
-    // rows that failed verification finish as one serial chain each (the
-    // schedules of launch_serial: small LDS slots when many chains share a
-    // CU; 4 KiB slots measured no different here)
-    if (dtype == MC_F8) {
-      k_fspec_rows<double><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, fail + c0);
-      if (g >= 256) k_scan_serial<MC_F8, MC_F8, true, 8192, 16><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
-      else k_scan_serial<MC_F8, MC_F8, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
-    } else {
-      k_fspec_rows<float><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, fail + c0);
-      if (g >= 256) k_scan_serial<MC_F4, MC_F4, true, 8192, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
-      else k_scan_serial<MC_F4, MC_F4, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, dtype, fail + c0);
-    }
+    launch_fspec_rows_any(sc, src_stride, dc, dst_stride, n, astype, dtype, fail + c0, g, st);
   }
   return mc_last_launch();
 }
