@@ -225,6 +225,167 @@ void launch_c4r_reduce(int R, unsigned grid, const uint8_t *s, uint32_t *ws, uin
   else k_c4r_reduce<8, NT><<<grid, MC_BLOCK, 0, st>>>(s, ws, ticket, p, wg0, ntiles, GT, ts);
 }
 
+// ---------------------------------------------------------------------------
+// ONE-launch decode with a lag: workgroup w reduces tile pair w and then
+// applies tile pair w - LAG.  The pair it applies was reduced LAG workgroups
+// earlier (in dispatch order), so its encoded planes were read ~LAG * 16 KiB
+// ago: an Infinity-Cache hit while LAG * 48 KiB of traffic stays well under
+// 256 MiB; and every total the apply needs (the groups before its own, the
+// earlier tiles of its group) was published by workgroups dispatched before
+// it.  Totals are published as 64-bit words (epoch << 32) | total in a
+// persistent per-stream state buffer (zeroed once; `epoch` differs per
+// call), so nothing needs resetting and stale words never match.  A wait
+// past the spin bound (a predecessor not yet dispatched: never with in-order
+// dispatch) falls back to computing the missing tile totals from the data.
+// ---------------------------------------------------------------------------
+MC_DEV uint32_t c41_tile_total_from_data(const uint8_t *src, const C4Params &p, size_t tile, uint32_t *red) {
+  // block-wide sum of one tile's deltas (fallback only)
+  uint32_t v[C4_PER];
+  const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  uint32_t a = 0;
+  if (e0 < p.n) {
+    mall_load_deltas<false>(src, p.n, e0, v);
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) a += v[k];
+  }
+  uint32_t tot;
+  (void)mc_block_excl_scan32(a, red, &tot);
+  return tot;
+}
+
+template <int SPINS>
+MC_DEV bool c41_wait(const unsigned long long *w, uint32_t epoch, uint32_t &val) {
+  for (int i = 0; i < SPINS; ++i) {
+    const unsigned long long x = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(x >> 32) == epoch) {
+      val = (uint32_t)x;
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                        unsigned long long *state, uint32_t *ticket, C4Params p,
+                                                        size_t ntiles, size_t npairs, unsigned GT, unsigned lag,
+                                                        uint32_t epoch) {
+  __shared__ uint32_t lds[2][MC_BLOCK / 64];
+  __shared__ uint32_t red[2][MC_BLOCK / 64];
+  __shared__ uint32_t fb[1];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * 4];
+  unsigned long long *tile_st = state, *grp_st = state + ntiles;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t w = blockIdx.x;
+  // ---- reduce pair w
+  if (w < npairs) {
+    const size_t t0 = 2 * w;
+    const size_t e0 = t0 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+    uint32_t acc[2] = {0, 0};
+    uint32_t v[2][C4_PER];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (e0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+        for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+      }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      acc[0] += __shfl_xor(acc[0], off, 64);
+      acc[1] += __shfl_xor(acc[1], off, 64);
+    }
+    if (lane == 0) {
+      lds[0][wave] = acc[0];
+      lds[1][wave] = acc[1];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (int h = 0; h < 2; ++h) {
+        uint32_t a = 0;
+        for (int q = 0; q < MC_BLOCK / 64; ++q) a += lds[h][q];
+        if (t0 + h < ntiles)
+          __hip_atomic_store(tile_st + t0 + h, ((unsigned long long)epoch << 32) | a, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        tot += a;
+      }
+      const size_t g = t0 / GT;
+      const size_t in_group = ntiles - g * GT < GT ? ntiles - g * GT : GT;
+      const unsigned long long arrivals = (in_group + 1) / 2;
+      unsigned long long *word = reinterpret_cast<unsigned long long *>(ticket + (size_t)MC_ARRIVAL_LINE * g);
+      const unsigned long long old = atomicAdd(word, ((unsigned long long)tot << 16) | 1ull);
+      if ((old & 0xffffu) + 1u == arrivals) {
+        __hip_atomic_store(grp_st + g, ((unsigned long long)epoch << 32) | (uint32_t)((uint32_t)(old >> 16) + tot),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *word = 0;
+      }
+    }
+  }
+  if (w < lag) return;
+  // ---- apply pair w - lag (both tiles)
+  const size_t q = w - lag;
+  const size_t g = (2 * q) / GT, gt0 = g * GT;
+  for (int h = 0; h < 2; ++h) {
+    const size_t tile = 2 * q + h;
+    if (tile >= ntiles) break;
+    uint32_t v[C4_PER];
+    const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+    if (e0 < p.n) {
+      mall_load_deltas<false>(src, p.n, e0, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+    }
+    // prefix pieces: groups before g (wave 0) and this group's tiles before `tile`
+    uint32_t x = 0;
+    bool ok = true;
+    if (wave == 0 && (size_t)lane < g) ok = c41_wait<4096>(grp_st + lane, epoch, x);
+    for (unsigned j = threadIdx.x; j < GT && gt0 + j < tile; j += MC_BLOCK) {
+      uint32_t y = 0;
+      ok = c41_wait<4096>(tile_st + gt0 + j, epoch, y) && ok;
+      x += y;
+    }
+    if (threadIdx.x == 0) fb[0] = 0;
+    __syncthreads();
+    if (!ok) atomicOr(&fb[0], 1u);
+    __syncthreads();
+    if (fb[0]) {  // fallback: the whole prefix from the data (never expected)
+      x = 0;
+      uint32_t tot = 0;
+      for (size_t t = 0; t < tile; ++t) tot += c41_tile_total_from_data(src, p, t, red[0]);
+      if (threadIdx.x == 0) x = tot;
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) {
+      run += v[k];
+      v[k] = run;
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 63) red[0][wave] = incl;
+    if (lane == 0) red[1][wave] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int ww = 0; ww < MC_BLOCK / 64; ++ww) {
+      if (ww < wave) pre += red[0][ww];
+      pre += red[1][ww];
+    }
+    c4_finish<MC_F4, MC_I2>(dst, tile, v, pre + (incl - run), outb, p);
+    __syncthreads();  // outb and red are reused by the second tile
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -299,6 +460,31 @@ int mc_lab_c4_decode_2l(const void *src, void *dst, size_t n, double scale, doub
     if (flags & 4) k_c4r_apply<false><<<(unsigned)(t1 - t0), MC_BLOCK, 0, st>>>(s, d, ws, p, t0, ntiles, GT);
     else k_c4r_apply<true><<<(unsigned)(t1 - t0), MC_BLOCK, 0, st>>>(s, d, ws, p, t0, ntiles, GT);
   }
+  return mc_last_launch();
+}
+
+// One-launch lag decode (above).  state: (ntiles + 64) 64-bit words, zeroed
+// once and kept per stream; epoch: a different nonzero value per call;
+// ticket: MC_ARRIVAL_WORDS zeroed words, left zero; lag in tile pairs.
+size_t mc_lab_c41_state_bytes(size_t n) {
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  return (ntiles + 64) * 8;
+}
+
+int mc_lab_c4_decode_1l(const void *src, void *dst, size_t n, double scale, double offset, void *state,
+                        size_t state_bytes, uint32_t *ticket, unsigned lag, uint32_t epoch, mc_stream_t stream) {
+  if (n == 0) return MC_OK;
+  if (!c4_ok(src, dst, n, MC_F4, MC_I2) || !ticket || !epoch || lag == 0) return MC_EINVAL;
+  if (!state || state_bytes < mc_lab_c41_state_bytes(n)) return MC_ENOSPC;
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const size_t npairs = (ntiles + 1) / 2;
+  unsigned GT = 256;
+  while ((ntiles + GT - 1) / GT > 64) GT *= 2;
+  if (GT > 1024) return MC_EINVAL;
+  k_c41_decode<<<(unsigned)(npairs + lag), MC_BLOCK, 0, (hipStream_t)stream>>>(
+      static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), static_cast<unsigned long long *>(state),
+      ticket, p, ntiles, npairs, GT, lag, epoch);
   return mc_last_launch();
 }
 
