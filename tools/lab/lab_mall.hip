@@ -277,20 +277,32 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restri
   unsigned long long *tile_st = state, *grp_st = state + ntiles;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t w = blockIdx.x;
+  const bool do_reduce = w < npairs, do_apply = w >= lag;
+  const size_t q = do_apply ? w - lag : 0;
+  // every load of both halves issued up front: the reduce pair's planes and
+  // the apply pair's (8 x 16 B per thread in flight)
+  uint32_t rv[2][C4_PER], av[2][C4_PER];
+  const size_t re0 = 2 * w * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+  const size_t ae0 = 2 * q * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (do_reduce && re0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<false>(src, p.n, re0 + h * MC_SCAN_TILE, rv[h]);
+    if (do_apply && ae0 + h * MC_SCAN_TILE < p.n) {
+      mall_load_deltas<false>(src, p.n, ae0 + h * MC_SCAN_TILE, av[h]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) av[h][k] = 0;
+    }
+  }
   // ---- reduce pair w
-  if (w < npairs) {
+  if (do_reduce) {
     const size_t t0 = 2 * w;
-    const size_t e0 = t0 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
     uint32_t acc[2] = {0, 0};
-    uint32_t v[2][C4_PER];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      if (e0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+      if (re0 + h * MC_SCAN_TILE < p.n) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (e0 + h * MC_SCAN_TILE < p.n) {
-#pragma unroll
-        for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+        for (int k = 0; k < C4_PER; ++k) acc[h] += rv[h][k];
       }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -306,7 +318,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restri
       uint32_t tot = 0;
       for (int h = 0; h < 2; ++h) {
         uint32_t a = 0;
-        for (int q = 0; q < MC_BLOCK / 64; ++q) a += lds[h][q];
+        for (int qq = 0; qq < MC_BLOCK / 64; ++qq) a += lds[h][qq];
         if (t0 + h < ntiles)
           __hip_atomic_store(tile_st + t0 + h, ((unsigned long long)epoch << 32) | a, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -324,22 +336,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restri
       }
     }
   }
-  if (w < lag) return;
-  // ---- apply pair w - lag (both tiles)
-  const size_t q = w - lag;
+  if (!do_apply) return;
+  // ---- apply pair q = w - lag (both tiles)
   const size_t g = (2 * q) / GT, gt0 = g * GT;
   for (int h = 0; h < 2; ++h) {
     const size_t tile = 2 * q + h;
     if (tile >= ntiles) break;
-    uint32_t v[C4_PER];
-    const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
-    if (e0 < p.n) {
-      mall_load_deltas<false>(src, p.n, e0, v);
-    } else {
-#pragma unroll
-      for (int k = 0; k < C4_PER; ++k) v[k] = 0;
-    }
-    // prefix pieces: groups before g (wave 0) and this group's tiles before `tile`
     uint32_t x = 0;
     bool ok = true;
     if (wave == 0 && (size_t)lane < g) ok = c41_wait<4096>(grp_st + lane, epoch, x);
@@ -361,8 +363,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restri
     uint32_t run = 0;
 #pragma unroll
     for (int k = 0; k < C4_PER; ++k) {
-      run += v[k];
-      v[k] = run;
+      run += av[h][k];
+      av[h][k] = run;
     }
     uint32_t incl = run;
 #pragma unroll
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c41_decode(const uint8_t *__restri
       if (ww < wave) pre += red[0][ww];
       pre += red[1][ww];
     }
-    c4_finish<MC_F4, MC_I2>(dst, tile, v, pre + (incl - run), outb, p);
+    c4_finish<MC_F4, MC_I2>(dst, tile, av[h], pre + (incl - run), outb, p);
     __syncthreads();  // outb and red are reused by the second tile
   }
 }
