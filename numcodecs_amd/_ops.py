@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -48,7 +49,7 @@ def workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
 
 
 class _VerifySlot:
-    """Per-(device, stream) resources of the one-launch checksum verify: a
+    """Per-(thread, device, stream) resources of the one-launch checksum verify: a
     zeroed arrival counter (left zero by every call), a reusable partials
     workspace and a verdict record in mapped, fine-grained pinned host memory
     (mc_verdict_alloc) that the kernel writes {computed, stored, seq} into;
@@ -68,6 +69,14 @@ class _VerifySlot:
             raise _native.MCodecError("the verdict record is not mapped into the device address space")
         self.seq = 0
         self.ws_sizes = {}
+
+    def __del__(self):
+        rec, self.rec = getattr(self, "rec", None), None
+        if rec:
+            try:
+                lib.mc_verdict_free(rec)
+            except Exception:  # interpreter shutdown
+                pass
 
     def next_seq(self) -> int:
         """The sequence word of the next verify (1 .. 2**32 - 1, never 0)."""
@@ -99,7 +108,10 @@ class _VerifySlot:
         return self.ws
 
 
-_VERIFY: "dict[tuple[int, int], _VerifySlot]" = {}
+# slots per thread (threading.local: a slot dies with its thread): two
+# threads verifying on the same stream must not share a verdict record, whose
+# words the host reads after its own kernel published them
+_TLS = threading.local()
 
 
 def arrival_ticket(t: torch.Tensor, st: int):
@@ -115,10 +127,13 @@ def _verify_slot(t: torch.Tensor, st: int):
     """The stream's verify slot, or None during HIP-graph capture."""
     if torch.cuda.is_current_stream_capturing():
         return None
+    slots = getattr(_TLS, "slots", None)
+    if slots is None:
+        slots = _TLS.slots = {}
     key = (t.device.index, st)
-    sl = _VERIFY.get(key)
+    sl = slots.get(key)
     if sl is None:
-        sl = _VERIFY[key] = _VerifySlot(t.device)
+        sl = slots[key] = _VerifySlot(t.device)
     return sl
 
 

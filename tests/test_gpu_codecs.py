@@ -548,7 +548,7 @@ def test_single_chunk_verify_one_launch(device, codec_id):
         y = torch.randint(0, 256, (100003,), dtype=torch.uint8, device=device)
         assert torch.equal(make().decode(make().encode(y)), y)
     torch.cuda.synchronize()
-    for sl in _ops._VERIFY.values():
+    for sl in _ops._TLS.slots.values():  # this thread's slots (default + side stream)
         assert not sl.ticket.any()
 
 
@@ -592,3 +592,32 @@ def test_foreign_device_arrays_are_used_in_place(device):
         assert np.array_equal(enc.cpu().numpy(), oracle.shuffle(xh, 4))
         d = Delta(dtype="<f4")
         assert np.array_equal(d.encode(obj).cpu().numpy().view("<f4"), oracle.delta_encode(xh, "<f4"))
+
+
+def test_checksum_decode_threadpool_same_stream(device):
+    """Verified decodes from several threads on the same (default) stream:
+    each thread has its own verdict record, so every call reads its own
+    verdict (a shared record would be overwritten by the next thread's
+    kernel before the first thread read it)."""
+    from numcodecs_amd import CRC32, Adler32
+
+    rng = np.random.default_rng(3)
+    bufs = [torch.from_numpy(rng.integers(0, 256, 1 << 20, dtype=np.uint8)).to(device) for _ in range(8)]
+    for make in (Fletcher32, CRC32, Adler32):
+        encs = [make().encode(b) for b in bufs]
+        bad = encs[5].clone()
+        bad[100] ^= 1
+
+        def work(i):
+            if i % 8 == 5:
+                try:
+                    make().decode(bad)
+                except RuntimeError:
+                    return "raised"
+                return "missed"
+            return bool(torch.equal(make().decode(encs[i % 8]), bufs[i % 8]))
+
+        with ThreadPool(6) as pool:
+            res = pool.map(work, range(48))
+        assert all(r is True for i, r in enumerate(res) if i % 8 != 5), make
+        assert all(r == "raised" for i, r in enumerate(res) if i % 8 == 5), make
