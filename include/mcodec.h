@@ -281,6 +281,26 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n,
  * `ticket`: MC_ARRIVAL_WORDS device words (8-B aligned), zero before the
  * first call and left zero (keep one per stream): the two-launch decode
  * (scan folded into the passes); NULL: the three-pass scan.  Same bytes. */
+/* The same chain over nchunks chunks of n elements (Zarr chunk pipelines):
+ * chunk c at src + c * src_stride / dst + c * dst_stride (strides 16-B
+ * multiples when nchunks > 1).  Encode: one pass (2-D grid of tiles x
+ * chunks); decode: a single pass per chunk segment with a running carry --
+ * one segment per chunk when nchunks >= 2048, else chunks are cut into
+ * segments whose totals a first pass computes (workspace:
+ * mc_fso_delta_shuffle_decode_batch_workspace, 0 when not needed).  Same
+ * bytes as the single-chunk calls per chunk. */
+int mc_fso_delta_shuffle_encode_batch(const void *src, size_t src_stride,
+                                      void *dst, size_t dst_stride,
+                                      size_t nchunks, size_t n, int dtype,
+                                      int astype, double offset, double scale,
+                                      mc_stream_t stream);
+size_t mc_fso_delta_shuffle_decode_batch_workspace(size_t nchunks, size_t n);
+int mc_fso_delta_shuffle_decode_batch(const void *src, size_t src_stride,
+                                      void *dst, size_t dst_stride,
+                                      size_t nchunks, size_t n, int astype,
+                                      int dtype, double scale, double offset,
+                                      void *workspace, size_t workspace_bytes,
+                                      mc_stream_t stream);
 size_t mc_fso_delta_shuffle_decode_workspace(size_t n);
 int mc_fso_delta_shuffle_decode(const void *src, void *dst, size_t n,
                                 int astype, int dtype, double scale,

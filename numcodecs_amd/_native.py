@@ -115,6 +115,14 @@ _SIGNATURES = {
     ],
     "mc_fso_delta_shuffle_encode": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp],
     "mc_fso_delta_shuffle_decode_workspace": [_c_size],
+    "mc_fso_delta_shuffle_encode_batch": [
+        _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp,
+    ],
+    "mc_fso_delta_shuffle_decode_batch_workspace": [_c_size, _c_size],
+    "mc_fso_delta_shuffle_decode_batch": [
+        _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size,
+        _c_vp,
+    ],
     "mc_fso_delta_shuffle_decode": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_double, _c_vp, _c_size, _c_vp, _c_vp,
     ],
@@ -155,6 +163,7 @@ _RESTYPES = {
     "mc_fletcher32_batch_workspace": ctypes.c_size_t,
     "mc_shuffle_fletcher32_workspace": ctypes.c_size_t,
     "mc_fso_delta_shuffle_decode_workspace": ctypes.c_size_t,
+    "mc_fso_delta_shuffle_decode_batch_workspace": ctypes.c_size_t,
     "mc_checksum32_workspace": ctypes.c_size_t,
 }
 

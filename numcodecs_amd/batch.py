@@ -45,6 +45,8 @@ __all__ = [
     "checksum32_decode_chunks",
     "fletcher32_encode_chunks",
     "fletcher32_decode_chunks",
+    "fso_delta_shuffle_encode_chunks",
+    "fso_delta_shuffle_decode_chunks",
 ]
 
 _CK_KINDS = {
@@ -116,6 +118,13 @@ def delta_chunks(chunks, delta, encode=True, out=None):
         )
     m = n * dst_t.itemsize
     out = torch.empty((b, m), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if not encode and b and nb >= _LARGE_ROW and rows.data_ptr() % 16 == 0 and \
+            rows.stride(0) % 16 == 0 and out.stride(0) % 16 == 0 and out.data_ptr() % 16 == 0:
+        # huge rows: each decoded by the whole chip (mc_delta_decode), not by
+        # one workgroup of the row kernel (16 x 64 MiB f4<-i2: 7.6 ms)
+        for i in range(b):
+            _ops.delta_decode(rows[i], out[i], n, delta.astype, delta.dtype)
+        return out
     if b and n:
         _ops.delta_batch(rows, rows.stride(0), out, out.stride(0), b, n, delta.dtype, delta.astype, encode)
     return out
@@ -423,7 +432,7 @@ def _fso_delta_shuffle_encode(fso, delta, sh, x):
     return out
 
 
-def _fso_delta_shuffle_decode(fso, delta, sh, x):
+def _fso_delta_shuffle_decode(fso, delta, sh, x, out=None):
     from .compat import torch_dtype
 
     sc4 = _c4_scalars(fso, delta, sh)
@@ -434,7 +443,8 @@ def _fso_delta_shuffle_decode(fso, delta, sh, x):
     if rem or n == 0 or n % 16 or raw.data_ptr() % 16:
         return None
     _, _, sc3, off4 = sc4
-    out = torch.empty(n * fso.dtype.itemsize, dtype=torch.uint8, device=raw.device)
+    if out is None:
+        out = torch.empty(n * fso.dtype.itemsize, dtype=torch.uint8, device=raw.device)
     _native.require_device()
     with torch.cuda.device(raw.device):
         ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_workspace(n), raw)
@@ -445,6 +455,68 @@ def _fso_delta_shuffle_decode(fso, delta, sh, x):
                                               _ops.arrival_ticket(raw, st), st),
               "mc_fso_delta_shuffle_decode")
     return out.view(torch_dtype(fso.dtype))
+
+
+# rows of at least _LARGE_ROW bytes decode row by row with the single-chunk
+# (multi-workgroup) decodes -- a row kernel would give each huge row one
+# workgroup (1 x 256 MiB of i2 Delta: 28 ms); for the fused FSO/Delta/Shuffle
+# chain only when there are at most _FEW_ROWS of them (more fill the chip
+# through the segmented batched decode)
+_FEW_ROWS = 4
+_LARGE_ROW = 16 << 20
+
+
+def fso_delta_shuffle_encode_chunks(rows, fso, delta, sh):
+    """[FixedScaleOffset, Delta, Shuffle(itemsize(astype))] encode of every row
+    of a [B, n * itemsize(dtype)] uint8 device batch in one launch
+    (mc_fso_delta_shuffle_encode_batch; each row its own Delta); returns the
+    [B, n * itemsize(astype)] encoded rows, or None when the chain or the
+    layout is not the fused kernels' (the caller then runs codec by codec)."""
+    sc4 = _c4_scalars(fso, delta, sh)
+    rows = _as_rows(rows)
+    b, nb = rows.shape
+    if sc4 is None or b == 0 or nb % fso.dtype.itemsize:
+        return None
+    n = nb // fso.dtype.itemsize
+    if n == 0 or n % 16 or rows.data_ptr() % 16 or (b > 1 and rows.stride(0) % 16):
+        return None
+    off, sc, _, _ = sc4
+    out = torch.empty((b, n * fso.astype.itemsize), dtype=torch.uint8, device=rows.device)
+    _native.require_device()
+    with torch.cuda.device(rows.device):
+        check(lib.mc_fso_delta_shuffle_encode_batch(rows.data_ptr(), rows.stride(0), out.data_ptr(), out.stride(0), b,
+                                                    n, _ops.dtype_code(fso.dtype), _ops.dtype_code(fso.astype), off,
+                                                    sc, _ops.stream(rows)), "mc_fso_delta_shuffle_encode_batch")
+    return out
+
+
+def fso_delta_shuffle_decode_chunks(rows, fso, delta, sh):
+    """Inverse of :func:`fso_delta_shuffle_encode_chunks`: every row (or, for
+    few large rows, every segment of a row) decoded in a single pass with a
+    running carry (mc_fso_delta_shuffle_decode_batch); [B, n * itemsize(dtype)]
+    rows, or None when not fusable."""
+    sc4 = _c4_scalars(fso, delta, sh)
+    rows = _as_rows(rows)
+    b, nb = rows.shape
+    if sc4 is None or b == 0 or nb % fso.astype.itemsize:
+        return None
+    n = nb // fso.astype.itemsize
+    if n == 0 or n % 16 or rows.data_ptr() % 16 or (b > 1 and rows.stride(0) % 16):
+        return None
+    _, _, sc3, off4 = sc4
+    out = torch.empty((b, n * fso.dtype.itemsize), dtype=torch.uint8, device=rows.device)
+    if b <= _FEW_ROWS and nb >= _LARGE_ROW and out.stride(0) % 16 == 0:
+        for i in range(b):  # each row alone fills the chip: the single-chunk two-launch decode
+            _fso_delta_shuffle_decode(fso, delta, sh, rows[i], out[i])
+        return out
+    _native.require_device()
+    with torch.cuda.device(rows.device):
+        ws = _ops.workspace(lib.mc_fso_delta_shuffle_decode_batch_workspace(b, n), rows)
+        check(lib.mc_fso_delta_shuffle_decode_batch(rows.data_ptr(), rows.stride(0), out.data_ptr(), out.stride(0), b,
+                                                    n, _ops.dtype_code(fso.astype), _ops.dtype_code(fso.dtype), sc3,
+                                                    off4, ws.data_ptr(), ws.numel(), _ops.stream(rows)),
+              "mc_fso_delta_shuffle_decode_batch")
+    return out
 
 
 def _bitround_shuffle(br: BitRound, x: torch.Tensor) -> torch.Tensor:

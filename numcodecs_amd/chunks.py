@@ -32,7 +32,7 @@ from . import _native, batch
 from .astype import AsType
 from .bitround import BitRound
 from .checksum32 import CRC32, CRC32C, Adler32, JenkinsLookup3
-from .compat import is_device_tensor
+from .compat import is_device_tensor, torch_dtype
 from .delta import Delta
 from .fixedscaleoffset import FixedScaleOffset
 from .fletcher32 import Fletcher32, _mismatch
@@ -145,14 +145,30 @@ def _decode_step(c, x: torch.Tensor, pending=None) -> torch.Tensor:
     return _per_row(c.decode, x)
 
 
+def _fused_c4_at(codecs, i):
+    """True when codecs[i:i+3] is FixedScaleOffset -> Delta -> Shuffle that the
+    fused kernels implement (batch._c4_scalars)."""
+    return i + 3 <= len(codecs) and batch._c4_scalars(*codecs[i:i + 3]) is not None
+
+
 def encode_chunks(codecs, chunks: torch.Tensor) -> torch.Tensor:
     """Encode every row of the device batch `chunks` ([B, ...], typed as the
-    first codec expects) through `codecs` in order; returns [B, m]."""
+    first codec expects) through `codecs` in order; returns [B, m].  A
+    FixedScaleOffset -> Delta -> Shuffle run encodes in one fused launch."""
     if not is_device_tensor(chunks) or chunks.dim() < 1:
         raise TypeError("encode_chunks takes a device tensor [B, ...]")
     x = chunks.reshape(chunks.shape[0], -1)
-    for c in list(codecs):
-        x = _encode_step(c, x)
+    codecs = list(codecs)
+    i = 0
+    while i < len(codecs):
+        if _fused_c4_at(codecs, i):
+            y = batch.fso_delta_shuffle_encode_chunks(_rows(x, x.shape[0]), *codecs[i:i + 3])
+            if y is not None:
+                x = y
+                i += 3
+                continue
+        x = _encode_step(codecs[i], x)
+        i += 1
     return x
 
 
@@ -162,8 +178,17 @@ def decode_chunks(codecs, chunks: torch.Tensor, _pending=None) -> torch.Tensor:
     if not is_device_tensor(chunks) or chunks.dim() < 1:
         raise TypeError("decode_chunks takes a device tensor [B, ...]")
     x = chunks.reshape(chunks.shape[0], -1)
-    for c in list(codecs)[::-1]:
-        x = _decode_step(c, x, _pending)
+    codecs = list(codecs)
+    i = len(codecs)
+    while i > 0:
+        if i >= 3 and _fused_c4_at(codecs, i - 3):
+            y = batch.fso_delta_shuffle_decode_chunks(_rows(x, x.shape[0]), *codecs[i - 3:i])
+            if y is not None:
+                x = y.view(torch_dtype(codecs[i - 3].dtype))  # typed as FixedScaleOffset.decode returns
+                i -= 3
+                continue
+        x = _decode_step(codecs[i - 1], x, _pending)
+        i -= 1
     return x
 
 

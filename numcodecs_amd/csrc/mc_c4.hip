@@ -22,11 +22,16 @@
 
 namespace {
 
+// blockIdx.y = chunk of a batch (row r at src + r * src_stride, dst + r *
+// dst_stride; one chunk: y = 0, strides unused)
 template <int D, int A, int STEPS = MC_SCAN_STEPS>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__ src,
-                                                    uint8_t *__restrict__ dst, C4Params p) {
+                                                    uint8_t *__restrict__ dst, C4Params p,
+                                                    size_t src_stride = 0, size_t dst_stride = 0) {
   constexpr int ES = A == MC_I2 || A == MC_U2 ? 2 : 4;
   constexpr int DS = D == MC_F4 ? 4 : 8;
+  src += (size_t)blockIdx.y * src_stride;
+  dst += (size_t)blockIdx.y * dst_stride;
   const size_t tile_e0 = (size_t)blockIdx.x * (4 * STEPS * MC_BLOCK);
   const int lane = threadIdx.x & 63;
   // all steps' loads first (n % 16 == 0: quads are whole)
@@ -124,6 +129,169 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply(const uint8_t *__restrict
   const uint32_t excl = mc_block_excl_scan32(run, red, &agg);
   const uint32_t tile_pre = (uint32_t)pair_pre[tile >> 1] + ((tile & 1) ? (uint32_t)first[tile >> 1] : 0u);
   c4_finish<D, A>(dst, tile, v, tile_pre + excl, outb, p);
+}
+
+// Batched decode (Zarr chunk pipelines): one workgroup per chunk walks its
+// tiles with a running carry -- a single pass, the next tile's planes in
+// flight while the current one is scanned and stored; thousands of chunks
+// fill the chip.  Same per-tile code as k_c4_apply.
+// Few large chunks would leave the chip under-filled with one workgroup per
+// chunk, so a chunk may be cut into `nseg` segments of whole tiles (grid =
+// chunks x segments): segment s starts from the sum of the earlier
+// segments' totals (seg_tot[c * nseg + s'], k_c4_seg_reduce) -- one extra
+// read of the encoded planes, in exchange for enough workgroups.
+template <int D, int A>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_seg_reduce(const uint8_t *__restrict__ src, size_t src_stride,
+                                                           uint32_t *__restrict__ seg_tot, unsigned nseg, C4Params p) {
+  constexpr int ES = c4_es<A>();
+  __shared__ uint32_t red[MC_BLOCK / 64];
+  const size_t c = blockIdx.x / nseg;
+  const unsigned sg = blockIdx.x - (unsigned)(c * nseg);
+  src += c * src_stride;
+  const size_t ntiles = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const size_t t0 = ntiles * sg / nseg, t1 = ntiles * (sg + 1) / nseg;
+  uint32_t acc = 0;
+  for (size_t t = t0; t < t1; t += 2) {  // two tiles' planes in flight
+    uint32_t v[2][C4_PER];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const size_t e0 = (t + h) * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+      if (t + h < t1 && e0 < p.n) {
+        load16_deltas<A, ES, false>(src, p.n, e0, v[h]);  // default policy: re-read by the decode pass
+      } else {
+#pragma unroll
+        for (int k = 0; k < C4_PER; ++k) v[h][k] = 0;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) acc += v[h][k];
+  }
+  uint32_t tot;
+  (void)mc_block_excl_scan32(acc, red, &tot);
+  if (threadIdx.x == 0) seg_tot[blockIdx.x] = tot;
+}
+
+template <int D, int A, bool NT>
+__global__ __launch_bounds__(MC_BLOCK) void k_c4_dec_rows(const uint8_t *__restrict__ src, size_t src_stride,
+                                                         uint8_t *__restrict__ dst, size_t dst_stride, C4Params p,
+                                                         const uint32_t *__restrict__ seg_tot = nullptr,
+                                                         unsigned nseg = 1) {
+  constexpr int DS = D == MC_F4 ? 4 : 8;
+  constexpr int ES = c4_es<A>();
+  __shared__ uint32_t red[MC_BLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * DS];
+  const size_t c = blockIdx.x / nseg;
+  const unsigned sg = blockIdx.x - (unsigned)(c * nseg);
+  src += c * src_stride;
+  dst += c * dst_stride;
+  const size_t ntiles_all = (p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const size_t tfirst = ntiles_all * sg / nseg, ntiles = ntiles_all * (sg + 1) / nseg;
+  uint32_t nxt[C4_PER];
+  auto load = [&](size_t tile, uint32_t (&v)[C4_PER]) {
+    const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
+    if (e0 < p.n) {
+      load16_deltas<A, ES, NT>(src, p.n, e0, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < C4_PER; ++k) v[k] = 0;
+    }
+  };
+  if (tfirst >= ntiles) return;
+  load(tfirst, nxt);
+  uint32_t carry = 0;
+  if (sg) {  // the earlier segments' totals, summed by the whole block
+    uint32_t x = 0;
+    for (unsigned j = threadIdx.x; j < sg; j += MC_BLOCK) x += seg_tot[c * nseg + j];
+    (void)mc_block_excl_scan32(x, red, &carry);
+  }
+  for (size_t t = tfirst; t < ntiles; ++t) {
+    uint32_t v[C4_PER];
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) v[k] = nxt[k];
+    if (t + 1 < ntiles) load(t + 1, nxt);
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < C4_PER; ++k) {
+      run += v[k];
+      v[k] = run;
+    }
+    uint32_t tot;
+    const uint32_t excl = mc_block_excl_scan32(run, red, &tot);
+    c4_finish<D, A>(dst, t, v, carry + excl, outb, p);
+    carry += tot;
+  }
+}
+
+template <int D, int A>
+static void c4_encode_batch(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, const C4Params &p,
+                            hipStream_t st) {
+  const unsigned tiles = (unsigned)((p.n + MC_SCAN_TILE - 1) / MC_SCAN_TILE);
+  for (size_t c0 = 0; c0 < nchunks; c0 += 65535) {
+    const unsigned rows = (unsigned)(nchunks - c0 < 65535 ? nchunks - c0 : 65535);
+    k_c4_enc<D, A><<<dim3(tiles, rows), MC_BLOCK, 0, st>>>(s + c0 * ss, d + c0 * ds, p, ss, ds);
+  }
+}
+
+// segments per chunk: enough workgroups to fill the chip (>= 2048), whole
+// tiles, none when the batch alone fills it
+static unsigned c4_batch_segments(size_t nchunks, size_t n) {
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  size_t seg = nchunks >= 2048 ? 1 : (2048 + nchunks - 1) / nchunks;
+  if (seg > ntiles) seg = ntiles;
+  if (seg > 4096) seg = 4096;
+  return (unsigned)(seg ? seg : 1);
+}
+
+// Segmented decodes run in groups of rows whose encoded planes the second
+// pass re-reads partly from the Infinity Cache (256 MiB MALL).  Measured on
+// 256 x 4 MiB / 16 x 64 MiB f4<-i2 (tools/probe_c4_batch.py): one group 414 /
+// 425 us; groups of 16 Mi elements 434 / 480 (more launch pairs); 64 Mi 364 /
+// 383; 128 Mi 360 / 363 (357 / 364 split evenly); 96 Mi and 192 Mi, with a
+// short last group, 403-450.  Default 128 Mi elements, split evenly
+// (MCODEC_C4_GROUP_MI overrides).
+struct C4Plan {
+  size_t rows;    // chunks per group (launch pair)
+  unsigned nseg;  // segments per chunk
+};
+
+static size_t c4_group_elems() {
+  static const size_t g = [] {
+    const char *e = getenv("MCODEC_C4_GROUP_MI");
+    const long v = e ? atol(e) : 0;
+    return (size_t)(v > 0 ? v : 128) << 20;
+  }();
+  return g;
+}
+
+static C4Plan c4_batch_plan(size_t nchunks, size_t n) {
+  if (c4_batch_segments(nchunks, n) == 1) return {nchunks, 1};
+  size_t g = c4_group_elems() / n;
+  if (g < 1) g = 1;
+  if (g > nchunks) g = nchunks;
+  const size_t ngroups = (nchunks + g - 1) / g;
+  g = (nchunks + ngroups - 1) / ngroups;  // even groups: a short last group costs a whole launch pair
+  const unsigned nseg = c4_batch_segments(g, n);
+  return nseg > 1 ? C4Plan{g, nseg} : C4Plan{nchunks, 1};
+}
+
+template <int D, int A>
+static void c4_decode_batch(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, const C4Params &p,
+                            uint32_t *seg_tot, hipStream_t st) {
+  const C4Plan plan = c4_batch_plan(nchunks, p.n);
+  const unsigned nseg = plan.nseg;
+  const size_t per_launch = nseg > 1 ? plan.rows : ((size_t)1 << 30);
+  for (size_t c0 = 0; c0 < nchunks; c0 += per_launch) {
+    const size_t rows = nchunks - c0 < per_launch ? nchunks - c0 : per_launch;
+    const unsigned grid = (unsigned)(rows * nseg);
+    if (nseg > 1) {  // segments: the second pass re-reads what the first read (default-policy loads)
+      k_c4_seg_reduce<D, A><<<grid, MC_BLOCK, 0, st>>>(s + c0 * ss, ss, seg_tot, nseg, p);
+      k_c4_dec_rows<D, A, false><<<grid, MC_BLOCK, 0, st>>>(s + c0 * ss, ss, d + c0 * ds, ds, p, seg_tot, nseg);
+    } else {
+      k_c4_dec_rows<D, A, true><<<grid, MC_BLOCK, 0, st>>>(s + c0 * ss, ss, d + c0 * ds, ds, p, seg_tot, nseg);
+    }
+  }
 }
 
 template <int D, int A>
@@ -302,6 +470,54 @@ int mc_fso_delta_shuffle_encode(const void *src, void *dst, size_t n, int dtype,
   uint8_t *d = static_cast<uint8_t *>(dst);
   hipStream_t st = (hipStream_t)stream;
   MC_C4_DISPATCH(c4_encode, s, d, p, st);
+  return mc_last_launch();
+}
+
+static bool c4_batch_ok(const void *src, size_t ss, const void *dst, size_t ds, size_t nchunks, size_t n, int dtype,
+                        int astype) {
+  if (!c4_ok(src, dst, n, dtype, astype)) return false;
+  if (nchunks > 1 && (ss % 16 || ds % 16 || ss < n * (size_t)mc_itemsize(dtype) ||
+                      ds < n * (size_t)mc_itemsize(astype)))
+    return false;
+  return true;
+}
+
+int mc_fso_delta_shuffle_encode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                                      size_t nchunks, size_t n, int dtype, int astype, double offset, double scale,
+                                      mc_stream_t stream) {
+  if (n == 0 || nchunks == 0) return MC_OK;
+  if (!c4_batch_ok(src, src_stride, dst, dst_stride, nchunks, n, dtype, astype)) return MC_EINVAL;
+  C4Params p;
+  p.n = n;
+  p.off = mc_num_f(offset);
+  p.sc = mc_num_f(scale);
+  p.rcp = 0.0;
+  p.fastdiv = false;
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  hipStream_t st = (hipStream_t)stream;
+  MC_C4_DISPATCH(c4_encode_batch, s, src_stride, d, dst_stride, nchunks, p, st);
+  return mc_last_launch();
+}
+
+size_t mc_fso_delta_shuffle_decode_batch_workspace(size_t nchunks, size_t n) {
+  const C4Plan plan = c4_batch_plan(nchunks, n);
+  return plan.nseg > 1 ? plan.rows * plan.nseg * sizeof(uint32_t) : 0;
+}
+
+int mc_fso_delta_shuffle_decode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
+                                      size_t nchunks, size_t n, int astype, int dtype, double scale, double offset,
+                                      void *workspace, size_t workspace_bytes, mc_stream_t stream) {
+  if (n == 0 || nchunks == 0) return MC_OK;
+  if (!c4_batch_ok(dst, dst_stride, src, src_stride, nchunks, n, dtype, astype)) return MC_EINVAL;
+  const size_t need = mc_fso_delta_shuffle_decode_batch_workspace(nchunks, n);
+  if (need && (!workspace || workspace_bytes < need || (uintptr_t)workspace % 4)) return MC_ENOSPC;
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  uint32_t *seg = static_cast<uint32_t *>(workspace);
+  hipStream_t st = (hipStream_t)stream;
+  MC_C4_DISPATCH(c4_decode_batch, s, src_stride, d, dst_stride, nchunks, p, seg, st);
   return mc_last_launch();
 }
 

@@ -218,3 +218,74 @@ def test_shuffle_fletcher32_fused_rows_vs_oracle(device, es):
     for i in range(b):
         assert dh[i].tobytes() == oracle.unshuffle(oracle.fletcher32_decode(eh[i, : n + 4]), es).tobytes()
 
+
+
+@pytest.mark.parametrize("dt,at,scale", [("<f4", "<i2", 1e3), ("<f8", "<u4", 1e6), ("<f4", "<i4", 3.7)])
+@pytest.mark.parametrize("n,b", [(4096 * 3, 5), (4096 * 64 + 48, 3), (16, 9)])
+def test_fused_c4_batch_vs_oracle(device, dt, at, scale, n, b):
+    """[FixedScaleOffset, Delta, Shuffle] over a batch runs the fused batched
+    kernels (one launch each way, a single-pass row decode); every row vs the
+    oracle chain, and the public batch functions on padded rows."""
+    codecs = [FixedScaleOffset(offset=1000, scale=scale, dtype=dt, astype=at), Delta(dtype=at),
+              Shuffle(np.dtype(at).itemsize)]
+    rng = np.random.default_rng(n + b)
+    xh = (1000.0 + rng.uniform(-15, 15, (b, n))).astype(dt)
+    x = torch.from_numpy(xh).to(device)
+    assert batch.fso_delta_shuffle_encode_chunks(x.view(torch.uint8), *codecs) is not None  # the fused path applies
+    enc = chunks.encode_chunks(codecs, x)
+    eh = enc.contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    for i in range(b):
+        assert eh[i].tobytes() == oracle_chain.chain_encode(codecs, xh[i]), i
+    dec = chunks.decode_chunks(codecs, enc)
+    assert dec.dtype == x.dtype
+    dh = dec.contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    for i in range(b):
+        assert dh[i].tobytes() == oracle_chain.chain_decode(codecs, eh[i].tobytes()), i
+    # padded rows (16-B multiple strides) through the batch functions
+    pad_in = torch.zeros((b, n * np.dtype(dt).itemsize + 64), dtype=torch.uint8, device=device)
+    pad_in[:, : n * np.dtype(dt).itemsize] = x.view(torch.uint8)
+    e2 = batch.fso_delta_shuffle_encode_chunks(pad_in[:, : n * np.dtype(dt).itemsize], *codecs)
+    assert torch.equal(e2, enc.view(torch.uint8).reshape(b, -1))
+    pad_enc = torch.zeros((b, e2.shape[1] + 32), dtype=torch.uint8, device=device)
+    pad_enc[:, : e2.shape[1]] = e2
+    d2 = batch.fso_delta_shuffle_decode_chunks(pad_enc[:, : e2.shape[1]], *codecs)
+    assert torch.equal(d2, dec.contiguous().view(torch.uint8).reshape(b, -1))
+
+
+@pytest.mark.parametrize("b,n", [(1, 4096 * 40 + 16), (3, 4096 * 7 + 32), (40, 4096 * 2)])
+def test_fused_c4_batch_segments_vs_oracle(device, b, n):
+    """Few chunks: the batched decode cuts each chunk into segments (a first
+    pass of segment totals); every row still equals the oracle."""
+    from numcodecs_amd._native import lib
+
+    codecs = [FixedScaleOffset(offset=1000, scale=1e3, dtype="<f4", astype="<i2"), Delta(dtype="<i2"), Shuffle(2)]
+    assert lib.mc_fso_delta_shuffle_decode_batch_workspace(b, n) > 0  # segmented
+    rng = np.random.default_rng(b * n)
+    xh = (1000.0 + rng.uniform(-15, 15, (b, n))).astype("<f4")
+    enc = chunks.encode_chunks(codecs, torch.from_numpy(xh).to(device))
+    eh = enc.contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    dh = chunks.decode_chunks(codecs, enc).contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    for i in range(b):
+        assert dh[i].tobytes() == oracle_chain.chain_decode(codecs, eh[i].tobytes()), i
+
+
+def test_few_large_rows_decode_row_by_row(device):
+    """Rows of at least batch._LARGE_ROW bytes (at most _FEW_ROWS for the chain) decode
+    row by row with the single-chunk decodes (the whole chip per row), both
+    for the fused [FixedScaleOffset, Delta, Shuffle] chain and for
+    batch.delta_chunks; vs the oracle."""
+    n = batch._LARGE_ROW // 2 + 16
+    b = 2
+    codecs = [FixedScaleOffset(offset=1000, scale=1e3, dtype="<f4", astype="<i2"), Delta(dtype="<i2"), Shuffle(2)]
+    rng = np.random.default_rng(5)
+    xh = (1000.0 + rng.uniform(-15, 15, (b, n))).astype("<f4")
+    enc = chunks.encode_chunks(codecs, torch.from_numpy(xh).to(device))
+    eh = enc.contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    dh = chunks.decode_chunks(codecs, enc).contiguous().view(torch.uint8).reshape(b, -1).cpu().numpy()
+    for i in range(b):
+        assert dh[i].tobytes() == oracle_chain.chain_decode(codecs, eh[i].tobytes()), i
+    d = Delta(dtype="<i4", astype="<i2")
+    eh2 = rng.integers(-300, 300, (b, n)).astype("<i2")
+    out = batch.delta_chunks(torch.from_numpy(eh2.view(np.uint8)).to(device), d, encode=False).cpu().numpy()
+    for i in range(b):
+        assert out[i].tobytes() == oracle.delta_decode(eh2[i], "<i4", "<i2").view(np.uint8).tobytes(), i
