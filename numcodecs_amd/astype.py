@@ -12,23 +12,28 @@ import numpy as np
 
 from . import _ops
 from .abc import Codec
-from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
+from .compat import device_out_bytes, empty_like_bytes, finish, ndarray_copy, to_dbuf
 from .quantize import _view_shape
 
 __all__ = ["AsType"]
 
 
-def _cast(buf, from_dt, to_dt):
+def _cast(buf, from_dt, to_dt, out=None):
+    """The cast, written straight into a device `out` when it can take it
+    (then `out` is returned, else the new array)."""
     src = to_dbuf(buf, flatten=False, contiguous=False)
     if src.nbytes % from_dt.itemsize:
         raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
     n = src.nbytes // from_dt.itemsize
     shape = _view_shape(src.shape, src.dtype.itemsize, from_dt.itemsize, src.order)
-    dst = empty_like_bytes(n * to_dt.itemsize, src)
+    direct = device_out_bytes(out, n * to_dt.itemsize, src)
+    dst = empty_like_bytes(n * to_dt.itemsize, src) if direct is None else direct
     if from_dt == to_dt:
         _ops.copy(src.data, dst, src.nbytes)
     else:
         _ops.cast(src.data, dst, n, from_dt, to_dt)
+    if direct is not None:
+        return out
     return finish(dst, to_dt, shape, src.order, src.host)
 
 
@@ -52,7 +57,8 @@ class AsType(Codec):
         return _cast(buf, self.decode_dtype, self.encode_dtype)
 
     def decode(self, buf, out=None):
-        return ndarray_copy(_cast(buf, self.encode_dtype, self.decode_dtype), out)
+        res = _cast(buf, self.encode_dtype, self.decode_dtype, out)
+        return res if res is out else ndarray_copy(res, out)
 
     def get_config(self):
         return {

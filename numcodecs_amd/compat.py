@@ -297,6 +297,29 @@ def empty_like_bytes(nbytes: int, like: DBuf) -> torch.Tensor:
     return torch.empty(nbytes, dtype=torch.uint8, device=like.data.device)
 
 
+def device_out_bytes(out, nbytes: int, like: DBuf) -> "torch.Tensor | None":
+    """The raw bytes of a caller's device `out` when a decode kernel can write
+    its result there directly instead of into a temporary that
+    :func:`ndarray_copy` then copies (same device as the input, contiguous in
+    C or F order, exactly `nbytes`, 16-B aligned, not overlapping the input):
+    the bytes land exactly where ndarray_copy would put them.  None sends
+    the result through ndarray_copy, which raises the reference's errors for
+    the other cases."""
+    if out is None or not is_device_tensor(out) or out.device != like.data.device or nbytes == 0:
+        return None
+    order = _tensor_order(out)
+    if order is None:
+        return None
+    flat = out.reshape(-1) if order == "C" else out.permute(*reversed(range(out.dim()))).reshape(-1)
+    if flat.numel() * flat.element_size() != nbytes:
+        return None
+    raw = flat.view(torch.uint8)
+    p, q = raw.data_ptr(), like.data.data_ptr()
+    if p % 16 or (p < q + like.nbytes and q < p + nbytes):
+        return None
+    return raw
+
+
 def finish(raw: torch.Tensor, dtype, shape, order: str, host: bool):
     """Present device bytes as the caller's kind of array.
 

@@ -11,7 +11,7 @@ import numpy as np
 
 from . import _ops
 from .abc import Codec
-from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
+from .compat import device_out_bytes, empty_like_bytes, finish, ndarray_copy, to_dbuf
 
 __all__ = ["Delta"]
 
@@ -75,8 +75,11 @@ class Delta(Codec):
                 f"Cannot cast ufunc 'add' output from {self.astype!r} to {self.dtype!r} "
                 "with casting rule 'same_kind'"
             )
-        dst = empty_like_bytes(n * self.dtype.itemsize, src)
+        direct = device_out_bytes(out, n * self.dtype.itemsize, src)
+        dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
         _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)
+        if direct is not None:
+            return out
         return ndarray_copy(finish(dst, self.dtype, (n,), "C", src.host), out)
 
     def get_config(self):

@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _ops
 from .abc import Codec
-from .compat import empty_like_bytes, finish, ndarray_copy, to_dbuf
+from .compat import device_out_bytes, empty_like_bytes, finish, ndarray_copy, to_dbuf
 
 __all__ = ["FixedScaleOffset"]
 
@@ -68,8 +68,11 @@ class FixedScaleOffset(Codec):
         n = src.nbytes // self.astype.itemsize
         t3, sc = _resolve(np.true_divide, self.astype, self.scale)
         t4, off = _resolve(np.add, t3, self.offset)
-        dst = empty_like_bytes(n * self.dtype.itemsize, src)
+        direct = device_out_bytes(out, n * self.dtype.itemsize, src)
+        dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
         _ops.fso_decode(src.data, dst, n, self.astype, t3, t4, self.dtype, sc, off)
+        if direct is not None:
+            return out
         return ndarray_copy(finish(dst, self.dtype, (n,), "C", src.host), out)
 
     def get_config(self):

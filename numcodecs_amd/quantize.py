@@ -12,7 +12,9 @@ import numpy as np
 
 from . import _ops
 from .abc import Codec
-from .compat import empty_like_bytes, finish, is_device_tensor, ndarray_copy, numpy_dtype, to_dbuf, torch_dtype
+from .compat import (
+    device_out_bytes, empty_like_bytes, finish, is_device_tensor, ndarray_copy, numpy_dtype, to_dbuf, torch_dtype,
+)
 
 __all__ = ["Quantize", "quantize_scale"]
 
@@ -66,8 +68,11 @@ class Quantize(Codec):
         if self.astype == self.dtype:
             dst = src.data
         else:
-            dst = empty_like_bytes(n * self.dtype.itemsize, src)
+            direct = device_out_bytes(out, n * self.dtype.itemsize, src)
+            dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
             _ops.cast(src.data, dst, n, self.astype, self.dtype)
+            if direct is not None:
+                return out
         return ndarray_copy(finish(dst, self.dtype, shape, src.order, src.host), out)
 
     def get_config(self):

@@ -621,3 +621,43 @@ def test_checksum_decode_threadpool_same_stream(device):
             res = pool.map(work, range(48))
         assert all(r is True for i, r in enumerate(res) if i % 8 != 5), make
         assert all(r == "raised" for i, r in enumerate(res) if i % 8 == 5), make
+
+
+@pytest.mark.parametrize("codec,dt_in", [
+    (Delta(dtype="<i4", astype="<i2"), "<i4"), (Delta(dtype="<f4"), "<f4"),
+    (FixedScaleOffset(offset=1000, scale=10, dtype="<f8", astype="<i4"), "<f8"),
+    (Quantize(digits=3, dtype="<f8", astype="<f4"), "<f8"),
+])
+@pytest.mark.parametrize("layout", ["C", "F", "misaligned", "overlap", "host"])
+def test_decode_into_device_out(device, codec, dt_in, layout):
+    """decode(buf, out=<device tensor>) writes the kernel's result straight
+    into `out` when it can (compat.device_out_bytes) and returns `out`; the
+    bytes equal decode() followed by ndarray_copy, also for an F-order `out`,
+    a misaligned one, one that overlaps the input, and a host input."""
+    from numcodecs_amd import compat
+
+    x = (np.arange(6000) % 97 * 1.5).astype(dt_in)
+    enc = codec.encode(torch.from_numpy(x).to(device))
+    ref = codec.decode(enc).contiguous().view(torch.uint8).reshape(-1)
+    nb = ref.numel()
+    tdt = compat.torch_dtype(codec.dtype)
+    if layout == "C":
+        out = torch.empty((60, 100), dtype=tdt, device=device)
+    elif layout == "F":
+        out = torch.empty((100, 60), dtype=tdt, device=device).t()
+    elif layout == "misaligned":
+        out = torch.empty(nb + 8, dtype=torch.uint8, device=device)[8:].view(tdt)
+    elif layout == "overlap":  # out is the encoded buffer itself when the widths agree
+        if enc.element_size() * enc.numel() != nb:
+            pytest.skip("widths differ")
+        out = enc.view(tdt)
+    else:
+        out = torch.empty(nb // np.dtype(codec.dtype).itemsize, dtype=tdt, device=device)
+        enc = enc.cpu().numpy()
+    res = codec.decode(enc, out=out)
+    assert res is out
+    if layout == "F":
+        got = out.t().contiguous().view(torch.uint8).reshape(-1)
+    else:
+        got = out.contiguous().view(torch.uint8).reshape(-1)
+    assert torch.equal(got, ref), (codec, layout)
