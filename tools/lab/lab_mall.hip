@@ -465,6 +465,60 @@ int mc_lab_c4_decode_2l(const void *src, void *dst, size_t n, double scale, doub
   return mc_last_launch();
 }
 
+// Two-stream slab pipeline: the reduce pass of slab k runs on `stream`, the
+// apply pass of slab k on `side` once reduce k is done, so reduce k+1 overlaps
+// apply k (no drained chip between slabs) and apply k re-reads planes read one
+// slab earlier (an Infinity-Cache hit while ~2 slabs of traffic fit in it).
+// window > 0: reduce k waits for apply k - window (bounds the reuse distance).
+// Slabs are whole groups, as in mc_lab_c4_decode_2l.  flags as there.
+int mc_lab_c4_decode_2s(const void *src, void *dst, size_t n, double scale, double offset, void *workspace,
+                        size_t workspace_bytes, uint32_t *ticket, int flags, int nslabs, int window,
+                        mc_stream_t stream, mc_stream_t side) {
+  if (n == 0) return MC_OK;
+  if (!c4_ok(src, dst, n, MC_F4, MC_I2) || !ticket || nslabs < 1 || nslabs > 64) return MC_EINVAL;
+  if (!workspace || workspace_bytes < mc_lab_c4_2l_workspace(n)) return MC_ENOSPC;
+  static hipEvent_t ev[2 * 64 + 1];
+  static bool init = false;
+  if (!init) {
+    for (auto &e : ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return MC_EHIP_BASE - 1;
+    init = true;
+  }
+  hipEvent_t *ev_r = ev, *ev_a = ev + 64, ev0 = ev[128];
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  hipStream_t st = (hipStream_t)stream, sd = (hipStream_t)side;
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  const int lr = (flags >> 4) & 3;
+  const int R = lr ? 1 << lr : 4;
+  unsigned GT = 256;
+  while ((ntiles + GT - 1) / GT > 64) GT *= 2;
+  if (GT > 1024) return MC_EINVAL;
+  const size_t ngroups = (ntiles + GT - 1) / GT;
+  uint32_t *ws = static_cast<uint32_t *>(workspace);
+  (void)hipEventRecord(ev0, st);
+  (void)hipStreamWaitEvent(sd, ev0, 0);
+  int last = -1;
+  for (int sl = 0; sl < nslabs; ++sl) {
+    const size_t g0 = ngroups * sl / nslabs, g1 = ngroups * (sl + 1) / nslabs;
+    if (g1 == g0) continue;
+    const size_t t0 = g0 * GT, t1 = g1 * GT < ntiles ? g1 * GT : ntiles;
+    if (window > 0 && sl >= window) (void)hipStreamWaitEvent(st, ev_a[sl - window], 0);
+    const unsigned grid = (unsigned)((t1 - t0 + R - 1) / R);
+    if (flags & 2) launch_c4r_reduce<false>(R, grid, s, ws, ticket, p, t0 / R, ntiles, GT, MC_ARRIVAL_LINE, st);
+    else launch_c4r_reduce<true>(R, grid, s, ws, ticket, p, t0 / R, ntiles, GT, MC_ARRIVAL_LINE, st);
+    (void)hipEventRecord(ev_r[sl], st);
+    (void)hipStreamWaitEvent(sd, ev_r[sl], 0);
+    if (flags & 4) k_c4r_apply<false><<<(unsigned)(t1 - t0), MC_BLOCK, 0, sd>>>(s, d, ws, p, t0, ntiles, GT);
+    else k_c4r_apply<true><<<(unsigned)(t1 - t0), MC_BLOCK, 0, sd>>>(s, d, ws, p, t0, ntiles, GT);
+    (void)hipEventRecord(ev_a[sl], sd);
+    last = sl;
+  }
+  if (last >= 0) (void)hipStreamWaitEvent(st, ev_a[last], 0);
+  return mc_last_launch();
+}
+
 // One-launch lag decode (above).  state: (ntiles + 64) 64-bit words, zeroed
 // once and kept per stream; epoch: a different nonzero value per call;
 // ticket: MC_ARRIVAL_WORDS zeroed words, left zero; lag in tile pairs.
