@@ -207,7 +207,11 @@ class _LibProxy:
     """Attribute access loads the library on first use (import stays cheap)."""
 
     def __getattr__(self, name):
-        return getattr(_load(), name)
+        # only reached on the first access of `name`: the function object is
+        # then cached on the proxy (a plain attribute hit per call afterwards)
+        fn = getattr(_load(), name)
+        self.__dict__[name] = fn
+        return fn
 
 
 lib = _LibProxy()

@@ -160,6 +160,27 @@ def copy(src: torch.Tensor, dst: torch.Tensor, nbytes: int) -> None:
         check(lib.mc_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream(src)), "mc_copy")
 
 
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
+def current_device_index(t: torch.Tensor) -> "int | None":
+    """`t`'s device index when it is a HIP tensor on the CURRENT device (the
+    case the fast paths handle without a device guard), else None."""
+    idx = t.get_device()
+    if idx < 0 or _cur_device is None or _raw_stream is None or idx != _cur_device():
+        return None
+    return idx
+
+
+def shuffle_ptr(idx: int, src_ptr: int, dst_ptr: int, nbytes: int, es: int, encode: bool) -> None:
+    """mc_shuffle / mc_unshuffle on raw device pointers of the current device
+    `idx` (torch's current stream there); the caller has validated sizes."""
+    fn = lib.mc_shuffle if encode else lib.mc_unshuffle
+    rc = fn(src_ptr, dst_ptr, nbytes, es, _raw_stream(idx))
+    if rc:
+        check(rc, "mc_shuffle" if encode else "mc_unshuffle")
+
+
 def shuffle(src: torch.Tensor, dst: torch.Tensor, nbytes: int, es: int, encode: bool) -> None:
     _native.require_device()
     if nbytes == 0:

@@ -10,6 +10,7 @@ import torch
 from . import _ops
 from .abc import Codec
 from .compat import (
+    _TORCH_TO_NP,
     empty_like_bytes,
     ensure_contiguous_ndarray,
     finish,
@@ -19,6 +20,9 @@ from .compat import (
 )
 
 __all__ = ["Shuffle"]
+
+# tensor dtypes the general path accepts (numpy equivalents exist)
+_DEVICE_DTYPES = frozenset(_TORCH_TO_NP)
 
 
 class Shuffle(Codec):
@@ -33,6 +37,9 @@ class Shuffle(Codec):
         self.elementsize = elementsize
 
     def _run(self, buf, out, encode):
+        res = self._run_device(buf, out, encode)
+        if res is not None:
+            return res
         src = to_dbuf(buf)  # ensure_contiguous_ndarray semantics (shuffle.py:24)
         nbytes = src.nbytes
         es = self.elementsize
@@ -65,6 +72,34 @@ class Shuffle(Codec):
         if out is not None:
             return ensure_contiguous_ndarray(out)
         return finish(res, np.uint8, (nbytes,), "C", src.host)
+
+    def _run_device(self, buf, out, encode):
+        """The common Zarr case on its own short path: a C-contiguous device
+        tensor in, a C-contiguous device tensor (or nothing) out, on the
+        current device -- the same checks, errors and results as the general
+        path below, without its normalisation steps (a 1 MiB chunk's codec
+        call is host-bound: BASELINE C1).  None: take the general path."""
+        es = self.elementsize
+        if not (type(buf) is torch.Tensor and es > 1 and buf.dtype in _DEVICE_DTYPES and buf.is_contiguous()):
+            return None
+        if out is not None and not (type(out) is torch.Tensor and out.is_cuda and out.is_contiguous()):
+            return None
+        idx = _ops.current_device_index(buf)
+        nbytes = buf.numel() * buf.element_size()
+        if idx is None or nbytes == 0:
+            return None
+        if nbytes % es != 0:  # shuffle.py:35-36
+            raise ValueError("Shuffle buffer is not an integer multiple of elementsize")
+        if out is None:
+            res = torch.empty(nbytes, dtype=torch.uint8, device=buf.device)
+        else:
+            res = out.reshape(-1)
+            if res.numel() * res.element_size() < nbytes:
+                raise ValueError("output buffer is too small for the shuffled data")
+            if res.get_device() != idx:
+                raise ValueError("out must be on the same device as the input")
+        _ops.shuffle_ptr(idx, buf.data_ptr(), res.data_ptr(), nbytes, es, encode)
+        return res
 
     def encode(self, buf, out=None):
         return self._run(buf, out, True)

@@ -139,6 +139,53 @@ def test_shuffle_out_argument(device):
     assert np.array_equal(outd.cpu().numpy(), oracle.shuffle(x, 4))
 
 
+@pytest.mark.parametrize("es", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("tdt", [torch.uint8, torch.int16, torch.float32, torch.float64, torch.bool])
+def test_shuffle_device_short_path(device, es, tdt):
+    """The device-tensor short path (Shuffle._run_device) against the oracle,
+    and its results, errors and return objects against the general path
+    (host staging of the same bytes)."""
+    nbytes = 48 * 4096 + 48
+    raw = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=device)
+    x = raw.view(tdt) if tdt is not torch.bool else (raw & 1).bool()
+    host = x.cpu().numpy()
+    codec = Shuffle(es)
+    assert codec._run_device(x, None, True) is not None  # the short path is the one exercised
+    enc = codec.encode(x)
+    assert enc.is_cuda and enc.dtype == torch.uint8 and enc.shape == (nbytes,)
+    assert np.array_equal(enc.cpu().numpy(), oracle.shuffle(host.view("u1"), es))
+    assert np.array_equal(enc.cpu().numpy(), codec.encode(host))
+    dec = codec.decode(enc)
+    assert torch.equal(dec, raw if tdt is not torch.bool else x.view(torch.uint8))
+    # out= of another dtype and shape: returns the flat view of out
+    out = torch.empty((nbytes // 4, 4), dtype=torch.uint8, device=device).view(torch.int32)
+    res = codec.encode(x, out=out)
+    assert res.data_ptr() == out.data_ptr() and res.shape == (out.numel(),) and res.dtype == torch.int32
+    assert torch.equal(res.view(torch.uint8), enc)
+    big = torch.zeros(nbytes + 64, dtype=torch.uint8, device=device)
+    codec.decode(enc, out=big)
+    assert torch.equal(big[:nbytes], dec.view(torch.uint8)) and not big[nbytes:].any()
+    with pytest.raises(ValueError, match="too small"):
+        codec.encode(x, out=torch.empty(nbytes - 1, dtype=torch.uint8, device=device))
+    with pytest.raises(ValueError, match="integer multiple"):
+        Shuffle(es).encode(raw[: es * 1000 + 1])
+
+
+def test_shuffle_device_general_path_cases(device):
+    """Inputs the short path hands to the general one (F order, an empty
+    tensor, elementsize <= 1, a non-contiguous out) keep the reference's
+    results and errors."""
+    x = torch.randn(64, 48, device=device)
+    xf = x.t()  # F-contiguous view
+    assert Shuffle(4)._run_device(xf, None, True) is None
+    assert np.array_equal(Shuffle(4).encode(xf).cpu().numpy(),
+                          oracle.shuffle(np.asfortranarray(xf.cpu().numpy()).reshape(-1, order="A"), 4))
+    assert Shuffle(4).encode(torch.empty(0, device=device)).numel() == 0
+    assert torch.equal(Shuffle(1).encode(x), x.view(-1).view(torch.uint8))
+    with pytest.raises(ValueError):
+        Shuffle(4).encode(x, out=torch.empty(2 * x.nbytes, dtype=torch.uint8, device=device)[::2])
+
+
 # ---------------------------------------------------------------------------
 # BitRound (test_bitround.py) -- bit-exact
 # ---------------------------------------------------------------------------
