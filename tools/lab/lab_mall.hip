@@ -122,7 +122,8 @@ void launch_apply(unsigned g, const uint8_t *s, uint8_t *d, const uint64_t *pre,
 template <int R, bool NT>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4r_reduce(const uint8_t *__restrict__ src, uint32_t *ws,
                                                         uint32_t *ticket, C4Params p, size_t wg0, size_t ntiles,
-                                                        unsigned GT, unsigned tstride) {
+                                                        unsigned GT, unsigned tstride,
+                                                        size_t nt_from = ~(size_t)0) {
   __shared__ uint32_t lds[R][MC_BLOCK / 64];
   uint32_t *tile_tot = ws, *gtot = ws + ntiles;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -132,7 +133,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4r_reduce(const uint8_t *__restri
   uint32_t v[R][C4_PER];
 #pragma unroll
   for (int h = 0; h < R; ++h)
-    if (e0 + h * MC_SCAN_TILE < p.n) mall_load_deltas<NT>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+    if (e0 + h * MC_SCAN_TILE < p.n) {
+      if (NT || t0 >= nt_from) mall_load_deltas<true>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+      else mall_load_deltas<false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+    }
 #pragma unroll
   for (int h = 0; h < R; ++h) {
     acc[h] = 0;
@@ -171,7 +175,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4r_reduce(const uint8_t *__restri
 template <bool NT>
 __global__ __launch_bounds__(MC_BLOCK) void k_c4r_apply(const uint8_t *__restrict__ src,
                                                        uint8_t *__restrict__ dst, const uint32_t *ws,
-                                                       C4Params p, size_t tile0, size_t ntiles, unsigned GT) {
+                                                       C4Params p, size_t tile0, size_t ntiles, unsigned GT,
+                                                       size_t nt_from = ~(size_t)0) {
   __shared__ uint32_t red[2][MC_BLOCK / 64];
   __shared__ __attribute__((aligned(16))) uint8_t outb[MC_SCAN_TILE * 4];
   const uint32_t *tile_tot = ws, *gtot = ws + ntiles;
@@ -185,7 +190,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4r_apply(const uint8_t *__restric
   uint32_t v[C4_PER];
   const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
   if (e0 < p.n) {
-    mall_load_deltas<NT>(src, p.n, e0, v);
+    if (NT || tile >= nt_from) mall_load_deltas<true>(src, p.n, e0, v);
+    else mall_load_deltas<false>(src, p.n, e0, v);
   } else {
 #pragma unroll
     for (int k = 0; k < C4_PER; ++k) v[k] = 0;
@@ -516,6 +522,32 @@ int mc_lab_c4_decode_2s(const void *src, void *dst, size_t n, double scale, doub
     last = sl;
   }
   if (last >= 0) (void)hipStreamWaitEvent(st, ev_a[last], 0);
+  return mc_last_launch();
+}
+
+// Two-launch decode (R = 2, one slab) with a per-tile load policy: the
+// reduce pass loads tiles >= r_nt_from nontemporally (default policy before),
+// the apply pass tiles >= a_nt_from.  The apply pass re-reads from the
+// Infinity Cache only what stayed there; tiles that would be evicted anyway
+// are read nt so they neither slow the reduce pass nor displace the others.
+int mc_lab_c4_decode_split(const void *src, void *dst, size_t n, double scale, double offset, void *workspace,
+                           size_t workspace_bytes, uint32_t *ticket, size_t r_nt_from, size_t a_nt_from,
+                           mc_stream_t stream) {
+  if (n == 0) return MC_OK;
+  if (!c4_ok(src, dst, n, MC_F4, MC_I2) || !ticket) return MC_EINVAL;
+  if (!workspace || workspace_bytes < mc_lab_c4_2l_workspace(n)) return MC_ENOSPC;
+  const C4Params p = c4_decode_params(n, scale, offset);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
+  unsigned GT = 256;
+  while ((ntiles + GT - 1) / GT > 64) GT *= 2;
+  if (GT > 1024) return MC_EINVAL;
+  uint32_t *ws = static_cast<uint32_t *>(workspace);
+  k_c4r_reduce<2, false><<<(unsigned)((ntiles + 1) / 2), MC_BLOCK, 0, st>>>(s, ws, ticket, p, 0, ntiles, GT,
+                                                                           MC_ARRIVAL_LINE, r_nt_from);
+  k_c4r_apply<false><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, ws, p, 0, ntiles, GT, a_nt_from);
   return mc_last_launch();
 }
 
