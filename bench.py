@@ -359,6 +359,19 @@ def config_workloads(dev, cpu, sets: int = 4) -> dict:
     out["cfg_C1"] = _cfg(2 * MiB / GiB / (t_e + t_d), t_e, t_d, 4 * MiB, "k_shuffle_enc<4> / k_shuffle_dec<4>",
                          cpu, "C1", "one 1 MiB chunk per codec call: launch/host-bound, not HBM-bound")
     del x1, e1, d1
+    # the same 1 MiB chunks as a Zarr pipeline hands them over: 256 per batched call
+    rows = 256
+    xb = [torch.randn(rows, MiB // 4, device=dev) for _ in range(sets)]
+    eb = [torch.empty(rows, MiB, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    db = [torch.empty(rows, MiB, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    t_be = _timed(lambda i: batch.shuffle_chunks(xb[i], 4, out=eb[i]), sets, 50)
+    t_bd = _timed(lambda i: batch.unshuffle_chunks(eb[i], 4, out=db[i]), sets, 50)
+    assert torch.equal(db[0].view(torch.float32), xb[0])
+    out["cfg_C1"]["batched_256"] = {
+        "GiBps": round(2 * rows * MiB / GiB / (t_be + t_bd), 1), "enc_us": round(t_be * 1e6, 1),
+        "dec_us": round(t_bd * 1e6, 1), "frac": round(4 * rows * MiB / (t_be + t_bd) / 1e9 / PEAK_GBPS, 4),
+        "note": "256 x 1 MiB chunks per batched call (numcodecs_amd.batch.shuffle_chunks / unshuffle_chunks)"}
+    del xb, eb, db
     # C2 f64 Shuffle(8)
     sh8 = Shuffle(8)
     x64 = [torch.randn(CHUNK // 8, device=dev, dtype=torch.float64) for _ in range(sets)]

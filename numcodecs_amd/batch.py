@@ -25,7 +25,7 @@ import torch
 from . import _native, _ops
 from ._native import check, lib
 from .bitround import BitRound, max_bits
-from .compat import ensure_contiguous_ndarray, is_device_tensor
+from .compat import device_out_bytes, ensure_contiguous_ndarray, is_device_tensor
 from .delta import Delta, check_first_elements
 from .fixedscaleoffset import FixedScaleOffset, _resolve
 from .fletcher32 import Fletcher32, _mismatch
@@ -368,12 +368,14 @@ class FilterPipeline:
                 i += 2
                 continue
             if i + 2 < len(cs) and is_device_tensor(x):
-                fused = _fso_delta_shuffle_decode(cs[i + 2], nxt, c, x)
+                # the chain's last stage decodes straight into a device `out`
+                direct = _c4_direct_out(cs[i + 2], x, out) if i + 3 == len(cs) else None
+                fused = _fso_delta_shuffle_decode(cs[i + 2], nxt, c, x, direct)
                 if fused is not None:
                     x = fused
                     i += 3
                     if i == len(cs):
-                        return ndarray_copy(x, out)
+                        return out if direct is not None else ndarray_copy(x, out)
                     continue
             if i == len(cs) - 1:
                 return c.decode(x, out=out)
@@ -430,6 +432,16 @@ def _fso_delta_shuffle_encode(fso, delta, sh, x):
                                               _ops.dtype_code(fso.dtype), _ops.dtype_code(fso.astype),
                                               off, sc, _ops.stream(raw)), "mc_fso_delta_shuffle_encode")
     return out
+
+
+def _c4_direct_out(fso, x, out):
+    """The raw bytes of a caller's device `out` when the fused decode of `x`
+    can write its result there (compat.device_out_bytes), else None."""
+    if out is None or not isinstance(fso, FixedScaleOffset):
+        return None
+    raw = _c4_raw(x)
+    n, rem = divmod(raw.numel(), fso.astype.itemsize)
+    return None if rem else device_out_bytes(out, n * fso.dtype.itemsize, raw)
 
 
 def _fso_delta_shuffle_decode(fso, delta, sh, x, out=None):

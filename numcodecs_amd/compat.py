@@ -259,6 +259,12 @@ def to_dbuf(buf, *, flatten=True, contiguous=True) -> DBuf:
             and buf.is_contiguous()):
         # the common case (an encoded chunk): flat device bytes, used as they are
         return DBuf(buf, _U8, (buf.numel(),), "C", False)
+    if type(buf) is torch.Tensor and buf.is_cuda and buf.is_contiguous() and buf.numel():
+        # a C-contiguous device array (a chunk to encode): its bytes in place
+        dtype = _TORCH_TO_NP.get(buf.dtype)
+        if dtype is not None:
+            shape = (buf.numel(),) if flatten else tuple(buf.shape)
+            return DBuf(buf.view(-1).view(torch.uint8), dtype, shape, "C", False)
     if not isinstance(buf, (torch.Tensor, np.ndarray, bytes, bytearray, memoryview)):
         dt = _device_array_as_tensor(buf)  # another library's device array: in place
         if dt is not None:
@@ -297,7 +303,7 @@ def empty_like_bytes(nbytes: int, like: DBuf) -> torch.Tensor:
     return torch.empty(nbytes, dtype=torch.uint8, device=like.data.device)
 
 
-def device_out_bytes(out, nbytes: int, like: DBuf) -> "torch.Tensor | None":
+def device_out_bytes(out, nbytes: int, like: "DBuf | torch.Tensor") -> "torch.Tensor | None":
     """The raw bytes of a caller's device `out` when a decode kernel can write
     its result there directly instead of into a temporary that
     :func:`ndarray_copy` then copies (same device as the input, contiguous in
@@ -305,7 +311,8 @@ def device_out_bytes(out, nbytes: int, like: DBuf) -> "torch.Tensor | None":
     the bytes land exactly where ndarray_copy would put them.  None sends
     the result through ndarray_copy, which raises the reference's errors for
     the other cases."""
-    if out is None or not is_device_tensor(out) or out.device != like.data.device or nbytes == 0:
+    data = like.data if isinstance(like, DBuf) else like  # the input's bytes
+    if out is None or not is_device_tensor(out) or out.device != data.device or nbytes == 0:
         return None
     order = _tensor_order(out)
     if order is None:
@@ -314,8 +321,8 @@ def device_out_bytes(out, nbytes: int, like: DBuf) -> "torch.Tensor | None":
     if flat.numel() * flat.element_size() != nbytes:
         return None
     raw = flat.view(torch.uint8)
-    p, q = raw.data_ptr(), like.data.data_ptr()
-    if p % 16 or (p < q + like.nbytes and q < p + nbytes):
+    p, q = raw.data_ptr(), data.data_ptr()
+    if p % 16 or (p < q + data.numel() * data.element_size() and q < p + nbytes):
         return None
     return raw
 

@@ -51,6 +51,40 @@ def test_fused_equals_sequential(device, dt, at, n):
     assert torch.equal(dec.view(torch.uint8).reshape(-1), dseq.view(torch.uint8).reshape(-1))
 
 
+@pytest.mark.parametrize("dt,at", [("<f4", "<i2"), ("<f8", "<u4")])
+def test_pipeline_decode_into_out(device, dt, at):
+    """FilterPipeline.decode(out=): a device `out` the fused decode can write
+    (contiguous C/F order, right size, 16-B aligned, not overlapping the
+    input) receives the result directly and is returned; any other `out`
+    goes through ndarray_copy with the reference's errors."""
+    n = 4096 * 9 + 16
+    x = (1000.0 + np.random.default_rng(7).uniform(-15, 15, n)).astype(dt)
+    pipe = batch.FilterPipeline(_chain(dt, at, 1000, 1e3 if np.dtype(at).itemsize == 2 else 1e6))
+    enc = pipe.encode(torch.from_numpy(x).to(device))
+    ref = pipe.decode(enc).view(torch.uint8).reshape(-1)
+    with np.errstate(all="ignore"):
+        oref = oracle.fso_decode(oracle.delta_decode(oracle.unshuffle(enc.cpu().numpy(), np.dtype(at).itemsize)
+                                                     .view(at), at), 1000, pipe.codecs[0].scale, dt, at)
+    assert np.array_equal(ref.cpu().numpy(), np.ascontiguousarray(oref).view("u1"))
+    tdt = torch.float32 if dt == "<f4" else torch.float64
+    for out in (torch.empty(n, dtype=tdt, device=device),
+                torch.empty((n // 16, 16), dtype=tdt, device=device).t(),  # F order
+                torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, device=device)):
+        out.zero_()
+        assert batch._c4_direct_out(pipe.codecs[0], enc, out) is not None
+        res = pipe.decode(enc, out=out)
+        assert res is out
+        flat = out.t().reshape(-1) if out.dim() == 2 else out.reshape(-1)
+        assert torch.equal(flat.view(torch.uint8), ref)
+    # not directly writable: misaligned, wrong size -> ndarray_copy semantics
+    big = torch.zeros(n * np.dtype(dt).itemsize + 4, dtype=torch.uint8, device=device)
+    mis = big[4:]
+    assert batch._c4_direct_out(pipe.codecs[0], enc, mis) is None
+    assert pipe.decode(enc, out=mis) is mis and torch.equal(mis, ref)
+    with pytest.raises(ValueError):
+        pipe.decode(enc, out=torch.empty(n + 1, dtype=tdt, device=device))
+
+
 def test_fusion_is_skipped_when_numpy_computes_elsewhere(device):
     """A strong numpy float64 offset makes numpy compute a float32 chunk in
     float64: the pipeline must not use the float32 fused kernel."""
