@@ -34,13 +34,14 @@ def dtype_code(dt) -> int:
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)  # the current device index
 
 
 def stream(t: torch.Tensor) -> int:
     """hipStream_t of torch's current stream on `t`'s device (the raw handle
     straight from torch's C++ side: the Python wrapper costs ~4 us a call)."""
     if _raw_stream is not None:
-        return _raw_stream(t.device.index)
+        return _raw_stream(t.get_device())
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
@@ -142,7 +143,7 @@ _NO_GUARD = contextlib.nullcontext()
 
 def _guard(t: torch.Tensor):
     """Make `t`'s device current for the call (a no-op when it already is)."""
-    if t.device.index == torch.cuda.current_device():
+    if t.get_device() == (_cur_device() if _cur_device is not None else torch.cuda.current_device()):
         return _NO_GUARD
     return torch.cuda.device(t.device)
 
@@ -158,9 +159,6 @@ def copy(src: torch.Tensor, dst: torch.Tensor, nbytes: int) -> None:
         raise ValueError("mc_copy copies within one device")
     with _guard(src):
         check(lib.mc_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream(src)), "mc_copy")
-
-
-_cur_device = getattr(torch._C, "_cuda_getDevice", None)
 
 
 def current_device_index(t: torch.Tensor) -> "int | None":
