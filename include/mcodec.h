@@ -202,6 +202,14 @@ int mc_fletcher32(const void *src, size_t nbytes, uint32_t *out_sum,
 int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes,
                          void *workspace, size_t workspace_bytes,
                          mc_stream_t stream);
+/* mc_fletcher32_encode in ONE launch: the checksum's last blocks fold the
+ * partials and write the footer (no finalize kernel).  `ticket` as for
+ * mc_fletcher32_verify_fused; NULL = mc_fletcher32_encode.  Workspace:
+ * mc_fletcher32_workspace(nbytes).  Replaces fletcher32.pyx:60-85
+ * (Fletcher32.encode) for one device chunk. */
+int mc_fletcher32_encode_fused(const void *src, void *dst, size_t nbytes,
+                               void *workspace, size_t workspace_bytes,
+                               uint32_t *ticket, mc_stream_t stream);
 /* out_pair (device, 2 words) = {fletcher32(src[0:nbytes-4]),
  * LE32(src[nbytes-4:nbytes])}; nbytes >= 4. */
 int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair,
@@ -360,6 +368,19 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride,
                                uint32_t *out_stored, void *workspace,
                                size_t workspace_bytes, mc_stream_t stream);
 
+/* Checksum32.encode of ONE chunk (checksum32.py:64-76) in one launch: the
+ * payload copy and the checksum in the tiles pass, the last block folds the
+ * tile partials and writes the 4 checksum bytes at `location` (and
+ * *out_sum if non-NULL).  `ticket` as for mc_fletcher32_verify_fused; NULL
+ * (or JenkinsLookup3, whose hash is one serial chain) = the batched entry
+ * point with nchunks = 1.  Workspace: mc_checksum32_workspace(kind, 1,
+ * chunk_bytes). */
+int mc_checksum32_encode_fused(int kind, const void *src, void *dst,
+                               size_t chunk_bytes, uint32_t init,
+                               const void *prefix, size_t prefix_bytes,
+                               int location, uint32_t *out_sum,
+                               void *workspace, size_t workspace_bytes,
+                               uint32_t *ticket, mc_stream_t stream);
 /* Checksum32.decode's verification of ONE encoded buffer (payload + 4 bytes
  * at `location`) in one launch: out_pair[0] = checksum of the payload,
  * out_pair[1] = the stored LE32 value (the caller compares and raises).

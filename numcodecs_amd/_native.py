@@ -100,6 +100,7 @@ _SIGNATURES = {
     "mc_fletcher32_workspace": [_c_size],
     "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],
+    "mc_fletcher32_encode_fused": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp, _c_vp],
     "mc_fletcher32_verify": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_verify_fused": [_c_vp, _c_size, _c_vp, _c_u32, _c_vp, _c_size, _c_vp, _c_vp],
     "mc_fletcher32_batch_workspace": [_c_size, _c_size],
@@ -137,6 +138,9 @@ _SIGNATURES = {
     "mc_checksum32_decode_batch": [
         _c_int, _c_vp, _c_size, _c_vp, _c_size, _c_size, _c_size, _c_u32, _c_vp, _c_size, _c_int,
         _c_vp, _c_vp, _c_vp, _c_size, _c_vp,
+    ],
+    "mc_checksum32_encode_fused": [
+        _c_int, _c_vp, _c_vp, _c_size, _c_u32, _c_vp, _c_size, _c_int, _c_vp, _c_vp, _c_size, _c_vp, _c_vp,
     ],
     "mc_checksum32_verify_fused": [
         _c_int, _c_vp, _c_size, _c_u32, _c_vp, _c_size, _c_int, _c_vp, _c_u32, _c_vp, _c_size, _c_vp, _c_vp,

@@ -311,11 +311,20 @@ def cast(src, dst, n, from_dt, to_dt) -> None:
 
 
 def fletcher32_encode(src, dst, nbytes) -> None:
+    """Payload copy + LE32 footer in one launch (the stream's arrival ticket;
+    the two-launch schedule during HIP-graph capture)."""
     _native.require_device()
     with _guard(src):
+        st = stream(src)
+        sl = _verify_slot(src, st)
+        if sl is not None:
+            ws = sl.workspace_for(("f32", nbytes), lambda: lib.mc_fletcher32_workspace(nbytes))
+            check(lib.mc_fletcher32_encode_fused(src.data_ptr(), dst.data_ptr(), nbytes, ws.data_ptr(), ws.numel(),
+                                                 sl.ticket.data_ptr(), st), "mc_fletcher32_encode_fused")
+            return
         ws = workspace(lib.mc_fletcher32_workspace(nbytes), src)
         check(lib.mc_fletcher32_encode(src.data_ptr(), dst.data_ptr(), nbytes, ws.data_ptr(),
-                                       ws.numel(), stream(src)), "mc_fletcher32_encode")
+                                       ws.numel(), st), "mc_fletcher32_encode")
 
 
 def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
@@ -374,11 +383,31 @@ def checksum32(kind, src, src_stride, nchunks, nbytes, init, prefix=None) -> tor
     return out[:nchunks]
 
 
+# Single-chunk Checksum32 encodes below this size finish in the tiles launch
+# (one launch: 1 MiB CRC32 / Adler32 encode 14.2 / 14.5 -> 10.5 / 8.3 us per
+# call); larger ones keep the separate finalize kernel, which measured ~3 us
+# faster on the GPU at 256 MiB (CRC32 99.9 vs 101.7-103.1 us: every block of
+# the fused copy drains its payload stores before it arrives).
+_CK_FUSED_ENCODE_MAX = 16 << 20
+
+
 def checksum32_encode(kind, src, src_stride, dst, dst_stride, nchunks, nbytes, init, location,
                       prefix=None) -> None:
-    """Checksum32.encode of `nchunks` rows into dst rows (LE32 footer at the start or end)."""
+    """Checksum32.encode of `nchunks` rows into dst rows (LE32 footer at the start or end).
+    One chunk of CRC32 / CRC32C / Adler32 below _CK_FUSED_ENCODE_MAX runs in one
+    launch (the stream's arrival ticket; the tiles-then-finalize schedule
+    during HIP-graph capture and for larger chunks)."""
     _native.require_device()
     with _guard(src):
+        if nchunks == 1 and kind != _native.MC_CK_JENKINS and nbytes < _CK_FUSED_ENCODE_MAX:
+            st = stream(src)
+            sl = _verify_slot(src, st)
+            if sl is not None:
+                ws = sl.workspace_for(("ck", kind, nbytes), lambda: lib.mc_checksum32_workspace(kind, 1, nbytes))
+                check(lib.mc_checksum32_encode_fused(kind, src.data_ptr(), dst.data_ptr(), nbytes, init & 0xFFFFFFFF,
+                                                     None, 0, location, None, ws.data_ptr(), ws.numel(),
+                                                     sl.ticket.data_ptr(), st), "mc_checksum32_encode_fused")
+                return
         pre = _prefix_dev(prefix, src)
         ws = workspace(lib.mc_checksum32_workspace(kind, nchunks, nbytes), src)
         check(lib.mc_checksum32_encode_batch(kind, src.data_ptr(), src_stride, dst.data_ptr(), dst_stride,

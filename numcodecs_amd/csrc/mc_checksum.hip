@@ -618,12 +618,10 @@ void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, 
                   size_t total, uint32_t *parts, const CrcFin &fin, const CkFinish *fx, hipStream_t st) {
   const unsigned cap = ck_grid_cap(COPY);
   const unsigned grid = (unsigned)(total < cap ? total : cap);
-  if constexpr (!COPY && ALS == ALD) {  // the fused finish serves the verify (no copy) only
-    if (fx) {
-      k_ck_tiles<KIND, K, COPY, ALS, ALD, true><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts,
-                                                                           fin, *fx);
-      return;
-    }
+  if (fx) {  // one chunk: the last block finishes it in this launch (verify, or encode with its copy)
+    k_ck_tiles<KIND, K, COPY, ALS, ALD, true><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts,
+                                                                         fin, *fx);
+    return;
   }
   k_ck_tiles<KIND, K, COPY, ALS, ALD, false><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts, fin,
                                                                         CkFinish{});
@@ -727,9 +725,8 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;
   uint32_t *parts = static_cast<uint32_t *>(ws);
-  // one chunk, no copy, with a ticket: finish in the tiles launch
-  // (ck_finish_chunk)
-  const bool fused = ticket && nchunks == 1 && !d;
+  // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
+  const bool fused = ticket && nchunks == 1;
   const CkFinish fx{init, seq, ticket, out, stored_out, footer, fs, stored};
   switch (K) {
 #define MC_CK_CASE(KK)                                                                         \
@@ -854,6 +851,22 @@ int mc_checksum32_decode_batch(int kind, const void *src, size_t src_stride, voi
 // out_pair[1] = the stored LE32 value; out_pair may be host-mapped pinned
 // memory.  `ticket`: one device word, zero before the first call, left zero
 // (keep one per stream); NULL = the two-launch path.
+int mc_checksum32_encode_fused(int kind, const void *src, void *dst, size_t chunk_bytes, uint32_t init,
+                               const void *prefix, size_t prefix_bytes, int location, uint32_t *out_sum,
+                               void *workspace, size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
+  if (!ticket || kind == MC_CK_JENKINS)  // Jenkins has no one-launch fold: the batched entry point
+    return mc_checksum32_encode_batch(kind, src, chunk_bytes, dst, chunk_bytes + 4, 1, chunk_bytes, init, prefix,
+                                      prefix_bytes, location, out_sum, workspace, workspace_bytes, stream);
+  if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
+  if (!dst || (chunk_bytes && !src) || (uintptr_t)ticket % 4) return MC_EINVAL;
+  if (prefix_bytes) return MC_EINVAL;  // a prefix belongs to Jenkins only
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  uint8_t *payload = location == MC_CK_START ? d + 4 : d;
+  uint8_t *footer = location == MC_CK_START ? d : d + chunk_bytes;
+  return ck_dispatch(kind, static_cast<const uint8_t *>(src), 0, payload, 0, 1, chunk_bytes, init, nullptr, 0,
+                     out_sum, footer, 0, nullptr, nullptr, workspace, workspace_bytes, (hipStream_t)stream, ticket, 0);
+}
+
 int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, uint32_t init,
                                const void *prefix, size_t prefix_bytes, int location, uint32_t *out_pair,
                                uint32_t seq, void *workspace, size_t workspace_bytes, uint32_t *ticket,

@@ -539,7 +539,8 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
   // nsl / grid slices (loads only, so a looping block keeps its loads in
   // flight); the two-level fold (64 shards) keeps the tail short
   const unsigned fg = f32_fused_grid();
-  const unsigned grid = tickets ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
+  // (the fused encode keeps one slice per block, as the two-launch copy does)
+  const unsigned grid = tickets && !dst ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
 #define MC_F32_U(CP, AL, U)                                                                   \
   do {                                                                                         \
     if (f32_ntld())                                                                            \
@@ -632,6 +633,14 @@ int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes, void *worksp
   if (!src || !dst || nbytes == 0) return MC_EINVAL;
   return f32_run(static_cast<const uint8_t *>(src), 0, static_cast<uint8_t *>(dst), 0, 1, nbytes,
                  F_FOOTER, nullptr, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int mc_fletcher32_encode_fused(const void *src, void *dst, size_t nbytes, void *workspace, size_t workspace_bytes,
+                               uint32_t *ticket, mc_stream_t stream) {
+  if (!ticket) return mc_fletcher32_encode(src, dst, nbytes, workspace, workspace_bytes, stream);
+  if (!src || !dst || nbytes == 0 || (uintptr_t)ticket % 4) return MC_EINVAL;
+  return f32_run(static_cast<const uint8_t *>(src), 0, static_cast<uint8_t *>(dst), 0, 1, nbytes, F_FOOTER, nullptr,
+                 workspace, workspace_bytes, (hipStream_t)stream, ticket, 0);
 }
 
 int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair, void *workspace,

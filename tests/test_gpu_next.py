@@ -279,3 +279,45 @@ def test_blosc_filters_sizes(device, mode):
             ref = blosc.blosc_filter(raw, ts, bs, mode)
             assert got.cpu().numpy().tobytes() == ref, (ts, nel, bs, mode)
             assert torch.equal(bsh.unshuffle(got, ts, bs, mode), xd), (ts, nel, bs, mode)
+
+
+@pytest.mark.parametrize("kind_name", ["crc32", "crc32c", "adler32", "fletcher32"])
+def test_one_launch_encode_abi(device, kind_name):
+    """mc_checksum32_encode_fused / mc_fletcher32_encode_fused (the payload
+    copy and the checksum footer in ONE launch) against the oracle, at both
+    footer locations, with and without a ticket (NULL = the two-launch
+    schedule), above and below the Python layer's size switch; the arrival
+    ticket is left zero."""
+    from numcodecs_amd import _native, _ops
+    from numcodecs_amd._native import lib
+
+    st = torch.cuda.current_stream(device).cuda_stream
+    ticket = torch.zeros(_native.MC_ARRIVAL_WORDS, dtype=torch.int32, device=device)
+    kinds = {"crc32": _native.MC_CK_CRC32, "crc32c": _native.MC_CK_CRC32C, "adler32": _native.MC_CK_ADLER32}
+    for n in (1, 17, 4096, 65537, (1 << 20) + 3, (17 << 20) + 5):
+        x = RNG.integers(0, 256, n, dtype=np.uint8)
+        xd = torch.from_numpy(x).to(device)
+        if kind_name == "fletcher32":
+            ref = np.frombuffer(oracle.fletcher32_encode(x), dtype=np.uint8)
+            for tk in (ticket.data_ptr(), None):
+                dst = torch.full((n + 4,), 0xAB, dtype=torch.uint8, device=device)
+                ws = torch.empty(max(lib.mc_fletcher32_workspace(n), 16), dtype=torch.uint8, device=device)
+                _native.check(lib.mc_fletcher32_encode_fused(xd.data_ptr(), dst.data_ptr(), n, ws.data_ptr(),
+                                                             ws.numel(), tk, st))
+                assert np.array_equal(dst.cpu().numpy(), ref), (n, tk)
+            continue
+        kind = kinds[kind_name]
+        for loc_name, loc in (("start", _native.MC_CK_START), ("end", _native.MC_CK_END)):
+            ref = oracle.checksum32_encode(kind_name, x, location=loc_name)
+            for tk in (ticket.data_ptr(), None):
+                dst = torch.full((n + 4,), 0xAB, dtype=torch.uint8, device=device)
+                out = torch.zeros(1, dtype=torch.int32, device=device)
+                ws = torch.empty(max(lib.mc_checksum32_workspace(kind, 1, n), 16), dtype=torch.uint8, device=device)
+                _native.check(lib.mc_checksum32_encode_fused(kind, xd.data_ptr(), dst.data_ptr(), n, 1 if
+                                                             kind_name == "adler32" else 0, None, 0, loc,
+                                                             out.data_ptr(), ws.data_ptr(), ws.numel(), tk, st))
+                assert np.array_equal(dst.cpu().numpy(), ref), (n, loc_name, tk)
+                assert int(out.cpu().numpy().view(np.uint32)[0]) == REF[kind_name](x), (n, loc_name, tk)
+    torch.cuda.synchronize()
+    assert not ticket.any()
+    assert _ops._CK_FUSED_ENCODE_MAX < (17 << 20)  # both schedules ran through the codecs above
