@@ -761,7 +761,7 @@ static inline unsigned ds_group_tiles(size_t ntiles) {
   return gt;
 }
 
-template <int ES>
+template <int ES, bool NT = false>
 __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce_g(const uint8_t *__restrict__ src, size_t n,
                                                             uint32_t *ws, uint32_t *ticket, size_t ntiles,
                                                             unsigned GT) {
@@ -780,8 +780,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce_g(const uint8_t *__re
 #pragma unroll
     for (int h = 0; h < DS_GROUP; ++h) {
       const uint8_t *tb = src + (t0 + h) * TE * ES;
-      const mc_u32x4 w0 = mc_ld16<false>(tb + 16 * (size_t)threadIdx.x);
-      const mc_u32x4 w1 = mc_ld16<false>(tb + 16 * (size_t)(MC_BLOCK + threadIdx.x));
+      const mc_u32x4 w0 = mc_ld16<NT>(tb + 16 * (size_t)threadIdx.x);
+      const mc_u32x4 w1 = mc_ld16<NT>(tb + 16 * (size_t)(MC_BLOCK + threadIdx.x));
       const uint32_t d[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       uint32_t a = 0;
 #pragma unroll
@@ -798,8 +798,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce_g(const uint8_t *__re
 #pragma unroll
     for (int h = 0; h < DS_GROUP; ++h) {
       const size_t tb = (t0 + h) * TE;
-      ds_load_half<ES, false>(src, n, tb + (size_t)threadIdx.x * HALF, v[h], 0);
-      ds_load_half<ES, false>(src, n, tb + (size_t)(MC_BLOCK + threadIdx.x) * HALF, v[h], HALF);
+      ds_load_half<ES, NT>(src, n, tb + (size_t)threadIdx.x * HALF, v[h], 0);
+      ds_load_half<ES, NT>(src, n, tb + (size_t)(MC_BLOCK + threadIdx.x) * HALF, v[h], HALF);
     }
 #pragma unroll
     for (int h = 0; h < DS_GROUP; ++h) {
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_reduce_g(const uint8_t *__re
   }
 }
 
-template <int ES>
+template <int ES, bool NT = false>
 __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply_g(const uint8_t *__restrict__ src,
                                                            uint8_t *__restrict__ dst, size_t n, const uint32_t *ws,
                                                            size_t ntiles, unsigned GT) {
@@ -853,8 +853,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply_g(const uint8_t *__res
   const size_t ea0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * H;
   const size_t eb0 = tile * ds_tile<ES>() + (size_t)(MC_BLOCK + threadIdx.x) * H;
   T v[PER];
-  ds_load_half<ES, false>(src, n, ea0, v, 0);
-  ds_load_half<ES, false>(src, n, eb0, v, H);
+  ds_load_half<ES, NT>(src, n, ea0, v, 0);
+  ds_load_half<ES, NT>(src, n, eb0, v, H);
   T ra = 0, rb = 0;
 #pragma unroll
   for (int i = 0; i < H; ++i) {
@@ -907,9 +907,21 @@ template <int ES>
 static void launch_dscan_g(const uint8_t *s, uint8_t *d, size_t n, uint32_t *ws, uint32_t *ticket, hipStream_t st) {
   const size_t ntiles = (n + ds_tile<ES>() - 1) / ds_tile<ES>();
   const unsigned gt = ds_group_tiles(ntiles);
-  k_dscan_reduce_g<ES><<<(unsigned)((ntiles + DS_GROUP - 1) / DS_GROUP), MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles,
-                                                                                            gt);
-  k_dscan_apply_g<ES><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
+  const unsigned rg = (unsigned)((ntiles + DS_GROUP - 1) / DS_GROUP);
+  // load policy per pass, MCODEC_DSCAN_NT (A/B): bit 0 = nontemporal loads in
+  // the reduce pass, bit 1 in the apply pass.  Default 2: the reduce pass
+  // keeps default-policy loads (what the Infinity Cache retains serves the
+  // re-read; nt there: 256 MiB i1 / i2 / i4 decode 137 / 127 / 122 ->
+  // 150 / 138 / 131 us), the apply pass reads nontemporally (132 / 127 / 120
+  // us; tools/probe_dscan_nt.py, profiles/r02/probe_dscan_nt.json)
+  static const int ntm = [] {
+    const char *e = getenv("MCODEC_DSCAN_NT");
+    return e ? atoi(e) : 2;
+  }();
+  if (ntm & 1) k_dscan_reduce_g<ES, true><<<rg, MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles, gt);
+  else k_dscan_reduce_g<ES, false><<<rg, MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles, gt);
+  if (ntm & 2) k_dscan_apply_g<ES, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
+  else k_dscan_apply_g<ES, false><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
 }
 
 // MCODEC_DSCAN=0 selects the generic three-pass kernels (A/B)
