@@ -238,11 +238,28 @@ MC_DEV void ck_finish_chunk(const CrcFin &fin, const uint32_t *partials, size_t 
   const size_t lo = tiles_per_chunk * threadIdx.x / MC_BLOCK;
   const size_t hi = tiles_per_chunk * (threadIdx.x + 1) / MC_BLOCK;
   uint32_t result;
+  // The thread's tile partials are loaded CK_FOLD_BATCH at a time, all loads
+  // issued before the first use: folded one by one, every agent-scope (sc1)
+  // load waited for the previous one -- 16 serial round trips per thread, the
+  // bulk of the one-launch verify's 7-9 us tail.  Indices past `hi` re-read
+  // the last partial and are masked out, so the loads stay unconditional.
+  constexpr int CK_FOLD_BATCH = 16;
   if constexpr (KIND == K_ADLER) {
     uint64_t s1 = 0, s2 = 0;
-    for (size_t j = lo; j < hi; ++j) {
-      s1 += ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j)]);
-      s2 += ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j) + 1]);
+    for (size_t j0 = lo; j0 < hi; j0 += CK_FOLD_BATCH) {
+      uint32_t a[CK_FOLD_BATCH], b[CK_FOLD_BATCH];
+#pragma unroll
+      for (int u = 0; u < CK_FOLD_BATCH; ++u) {
+        const size_t j = j0 + u < hi ? j0 + u : hi - 1;
+        a[u] = ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j)]);
+        b[u] = ck_ld<SC1>(&partials[2 * (c * tiles_per_chunk + j) + 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < CK_FOLD_BATCH; ++u)
+        if (j0 + u < hi) {
+          s1 += a[u];
+          s2 += b[u];
+        }
     }
     s1 = wave_sum(s1 % ADLER_P);
     s2 = wave_sum(s2 % ADLER_P);
@@ -276,10 +293,16 @@ MC_DEV void ck_finish_chunk(const CrcFin &fin, const uint32_t *partials, size_t 
     }
     __syncthreads();
     uint32_t acc = 0;
-#pragma unroll 4
-    for (size_t j = lo; j < hi; ++j)
-      acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
-            ck_ld<SC1>(&partials[c * tiles_per_chunk + j]);
+    for (size_t j0 = lo; j0 < hi; j0 += CK_FOLD_BATCH) {
+      uint32_t v[CK_FOLD_BATCH];
+#pragma unroll
+      for (int u = 0; u < CK_FOLD_BATCH; ++u)
+        v[u] = ck_ld<SC1>(&partials[c * tiles_per_chunk + (j0 + u < hi ? j0 + u : hi - 1)]);
+#pragma unroll
+      for (int u = 0; u < CK_FOLD_BATCH; ++u)
+        if (j0 + u < hi)
+          acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^ v[u];
+    }
     if (hi > lo) acc = gf_mul(acc, fin.tail[threadIdx.x], crc_poly<KIND>());
     acc = wave_xor(acc);
     if (lane == 0) red[0][wave] = acc;
