@@ -217,7 +217,7 @@ int mc_fletcher32_verify(const void *src, size_t nbytes, uint32_t *out_pair,
                          mc_stream_t stream);
 /* mc_fletcher32_verify in ONE launch: the checksum's last blocks fold the
  * partials (no finalize kernel).  `ticket`: MC_ARRIVAL_WORDS device uint32
- * words (an arrival counter), zero before the first call and left zero by every call
+ * words (an arrival counter, 8-B aligned), zero before the first call and left zero by every call
  * (keep one per stream); NULL = mc_fletcher32_verify (seq must be 0).
  * out_rec = {computed, stored, seq, -}: with seq != 0 the kernel writes
  * out_rec[2] = seq after the verdict, so with out_rec = the device address of

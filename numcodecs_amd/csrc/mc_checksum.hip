@@ -347,6 +347,20 @@ struct CkFinish {
   const uint8_t *stored;
 };
 
+// Adler32's one-launch finish needs no partial stores at all: a block's
+// tiles add up (absolute weights), and its (S1, S2) mod P travel inside ONE
+// returning 64-bit atomic on its shard's word, packed as count (bits 0-7),
+// sum of S1 (8-31), sum of S2 (32-55) -- at most 255 blocks per shard keep
+// every field from carrying into the next.  The shard's last arriver holds
+// the shard's sums and adds them (mod P) into the top word the same way; the
+// top's last arriver finishes the chunk.  Each last arriver zeroes the word
+// it closed, so the ticket is left zero.  No vmcnt wait for hand-off stores,
+// no fold over per-tile partials.
+constexpr unsigned ADLER_MAX_GRID = MC_ARRIVAL_SHARDS * 255u;
+
+MC_DEV void adler_arrive_finish(uint32_t a1, uint32_t a2, size_t n, const uint8_t *src, size_t src_stride,
+                                const struct CkFinish &fx);
+
 template <int KIND, int K, bool COPY, int ALS, int ALD, bool FUSED>
 __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
     const uint8_t *__restrict__ src, size_t src_stride, uint8_t *__restrict__ dst,
@@ -365,6 +379,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
     g = crc_consts<KIND>().g[threadIdx.x];
     __syncthreads();
   }
+  uint32_t adl1 = 0, adl2 = 0;  // FUSED Adler32: the block's (S1, S2) mod P (thread 0)
   for (size_t tile = blockIdx.x; tile < total_tiles; tile += gridDim.x) {
     const size_t c = tile / tiles_per_chunk;
     const size_t t = tile - c * tiles_per_chunk;
@@ -432,9 +447,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
           y += red[1][w];
         }
         if constexpr (FUSED) {
-          __hip_atomic_store(&partials[2 * tile], (uint32_t)(x % ADLER_P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&partials[2 * tile + 1], (uint32_t)(y % ADLER_P), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          adl1 = (uint32_t)((adl1 + x) % ADLER_P);
+          adl2 = (uint32_t)((adl2 + y) % ADLER_P);
         } else {
           partials[2 * tile] = (uint32_t)(x % ADLER_P);
           partials[2 * tile + 1] = (uint32_t)(y % ADLER_P);
@@ -442,6 +456,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
       }
     }
     __syncthreads();  // red[] is reused by the next tile
+  }
+  if constexpr (FUSED && KIND == K_ADLER) {
+    if (threadIdx.x == 0) adler_arrive_finish(adl1, adl2, n, src, src_stride, fx);
+    return;
   }
   if constexpr (FUSED) {
     __shared__ uint32_t last;
@@ -458,6 +476,36 @@ __global__ __launch_bounds__(MC_BLOCK) void k_ck_tiles(
       mc_arrivals_reset(fx.ticket);  // left zero for the next launch
     }
   }
+}
+
+MC_DEV void adler_arrive_finish(uint32_t a1, uint32_t a2, size_t n, const uint8_t *src, size_t src_stride,
+                                const CkFinish &fx) {
+  (void)src;
+  (void)src_stride;
+  const unsigned sh = mc_arrival_shard(blockIdx.x);
+  unsigned long long *w = reinterpret_cast<unsigned long long *>(fx.ticket + MC_ARRIVAL_LINE * sh);
+  const unsigned long long old =
+      atomicAdd(w, ((unsigned long long)a2 << 32) | ((unsigned long long)a1 << 8) | 1ull);
+  if ((old & 0xffu) + 1u != mc_arrival_per(sh, gridDim.x)) return;
+  *w = 0;  // every arrival of this shard is in
+  const uint32_t s1 = (uint32_t)((((old >> 8) & 0xffffffu) + a1) % ADLER_P);
+  const uint32_t s2 = (uint32_t)((((old >> 32) & 0xffffffu) + a2) % ADLER_P);
+  unsigned long long *t = reinterpret_cast<unsigned long long *>(fx.ticket + MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS);
+  const unsigned long long top =
+      atomicAdd(t, ((unsigned long long)s2 << 32) | ((unsigned long long)s1 << 8) | 1ull);
+  if ((top & 0xffu) + 1u != mc_arrival_nshards(gridDim.x)) return;
+  *t = 0;
+  const uint64_t x = (((top >> 8) & 0xffffffu) + s1) % ADLER_P;
+  const uint64_t y = (((top >> 32) & 0xffffffu) + s2) % ADLER_P;
+  // zlib.adler32(data, value): a0 = value & 0xffff, b0 = value >> 16
+  const uint64_t a0 = fx.init & 0xffffu, b0 = fx.init >> 16;
+  const uint64_t a = (a0 + x) % ADLER_P;
+  const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
+  const uint32_t result = (uint32_t)((b << 16) | a);
+  if (fx.stored_out) fx.stored_out[0] = load_le32(fx.stored);
+  if (fx.out) fx.out[0] = result;
+  if (fx.footer) store_le32(fx.footer, result);
+  mc_publish_verdict_seq(fx.out, fx.seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -642,8 +690,9 @@ void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, 
   const unsigned cap = ck_grid_cap(COPY);
   const unsigned grid = (unsigned)(total < cap ? total : cap);
   if (fx) {  // one chunk: the last block finishes it in this launch (verify, or encode with its copy)
-    k_ck_tiles<KIND, K, COPY, ALS, ALD, true><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts,
-                                                                         fin, *fx);
+    const unsigned fg = KIND == K_ADLER && grid > ADLER_MAX_GRID ? ADLER_MAX_GRID : grid;
+    k_ck_tiles<KIND, K, COPY, ALS, ALD, true><<<fg, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts,
+                                                                       fin, *fx);
     return;
   }
   k_ck_tiles<KIND, K, COPY, ALS, ALD, false><<<grid, MC_BLOCK, 0, st>>>(s, ss, d, ds, n, tpc, total, parts, fin,
@@ -881,7 +930,7 @@ int mc_checksum32_encode_fused(int kind, const void *src, void *dst, size_t chun
     return mc_checksum32_encode_batch(kind, src, chunk_bytes, dst, chunk_bytes + 4, 1, chunk_bytes, init, prefix,
                                       prefix_bytes, location, out_sum, workspace, workspace_bytes, stream);
   if (!valid_kind(kind) || (location != MC_CK_START && location != MC_CK_END)) return MC_EINVAL;
-  if (!dst || (chunk_bytes && !src) || (uintptr_t)ticket % 4) return MC_EINVAL;
+  if (!dst || (chunk_bytes && !src) || (uintptr_t)ticket % 8) return MC_EINVAL;
   if (prefix_bytes) return MC_EINVAL;  // a prefix belongs to Jenkins only
   uint8_t *d = static_cast<uint8_t *>(dst);
   uint8_t *payload = location == MC_CK_START ? d + 4 : d;
@@ -898,6 +947,7 @@ int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, 
   if (encoded_bytes < 4 || !src || !out_pair) return MC_EINVAL;
   // only the one-launch finish of CRC32 / CRC32C / Adler32 publishes `seq`
   if (seq && (!ticket || kind == MC_CK_JENKINS)) return MC_EINVAL;
+  if (ticket && (uintptr_t)ticket % 8) return MC_EINVAL;  // 64-bit arrival words (Adler32)
   if (prefix_bytes && (kind != MC_CK_JENKINS || !prefix)) return MC_EINVAL;
   const size_t n = encoded_bytes - 4;
   const uint8_t *s = static_cast<const uint8_t *>(src);

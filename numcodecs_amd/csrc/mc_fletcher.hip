@@ -189,6 +189,30 @@ MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t 
                              const uint8_t *src, size_t src_stride, uint8_t *dst, size_t dst_stride,
                              size_t nbytes, uint32_t *out, uint32_t seq = 0);
 
+// one-launch finish (k_f32_partial with `tickets`): the packed arrival word
+// {count, S1 sum, S2 sum, nonzero count}; at most 255 blocks per shard
+constexpr unsigned F32_MAX_FUSED_GRID = MC_ARRIVAL_SHARDS * 255u;
+MC_DEV unsigned long long f32_pack(uint32_t s1, uint32_t s2, bool nz) {
+  return ((unsigned long long)nz << 56) | ((unsigned long long)s2 << 32) | ((unsigned long long)s1 << 8) | 1ull;
+}
+
+// chunk c's checksum f to where `mode` puts it (F_SUM: out[c]; F_FOOTER: LE32
+// footer after the payload in dst, and out[c] if set; F_VERIFY: out[2c] = f,
+// out[2c+1] = the stored footer, then `seq` published)
+MC_DEV void f32_write_result(uint32_t f, size_t c, int mode, const uint8_t *src, size_t src_stride, uint8_t *dst,
+                             size_t dst_stride, size_t nbytes, uint32_t *out, uint32_t seq) {
+  if (mode == F_SUM) {
+    out[c] = f;
+  } else if (mode == F_FOOTER) {
+    store_le32(dst + c * dst_stride + nbytes, f);
+    if (out) out[c] = f;
+  } else {
+    out[2 * c] = f;
+    out[2 * c + 1] = load_le32(src + c * src_stride + nbytes);
+    mc_publish_verdict_seq(out, seq);
+  }
+}
+
 // block = (chunk c, slice sl), partials[block] = {S1, S2, nz}; or, with
 // `tickets` (one chunk, FUSED finish): block b sums slices b, b + grid, ...
 // (absolute weights: slice partials add; the launch gives one slice per
@@ -257,49 +281,31 @@ __global__ __launch_bounds__(MC_BLOCK) void k_f32_partial(
     }
     return;
   }
-  // fused finish in two levels, in this launch (no finalize kernel, no extra
-  // boundary): block b arrives in shard sh = b % 64 (mc_arrive_shard); the
-  // last block of a shard folds that shard's partials (shard-major:
-  // partials[sh * per_max + b / 64]) while other shards still stream, and the
-  // last of the shard folders (mc_arrive_top) finishes the chunk from the
-  // shard sums (partials[64 * per_max + sh]).
-  __shared__ uint32_t last;
+  // fused finish in this launch (no finalize kernel, no partial stores): the
+  // block's {S1 mod M, S2 mod M, nz} travel inside ONE returning 64-bit
+  // atomic on its shard's word (block b in shard b % 64), packed as count
+  // (bits 0-7), sum of S1 (8-31), sum of S2 (32-55), count of nonzero blocks
+  // (56-63) -- at most F32_MAX_FUSED_GRID blocks keep every field from
+  // carrying.  The shard's last arriver holds the shard's sums and adds them
+  // into the top word the same way; the top's last arriver finishes the
+  // chunk.  Each last arriver zeroes the word it closed (left zero).  (The
+  // previous form stored partials sc1, waited for the stores, arrived, and
+  // had the last blocks fold them: ~3 us more per verify.)
+  if (threadIdx.x != 0) return;
   const unsigned sh = mc_arrival_shard(blockIdx.x);
-  const unsigned per_max = (gridDim.x + MC_ARRIVAL_SHARDS - 1) / MC_ARRIVAL_SHARDS;
-  const unsigned per = mc_arrival_per(sh, gridDim.x);
-  if (threadIdx.x == 0) {
-    uint32_t *q = partials + 3 * ((size_t)sh * per_max + blockIdx.x / MC_ARRIVAL_SHARDS);
-    __hip_atomic_store(q + 0, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 2, nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = mc_arrive_shard(tickets, gridDim.x);
-  }
-  __syncthreads();
-  if (!last) return;
-  F32Part f;
-  part_init(f);
-  for (unsigned i = threadIdx.x; i < per; i += MC_BLOCK) {
-    const uint32_t *q = partials + 3 * ((size_t)sh * per_max + i);
-    f.s1 += part_ld<true>(q);
-    f.s2a += part_ld<true>(q + 1);  // partial S2 already reduced: s2b stays 0
-    f.nz |= part_ld<true>(q + 2);
-  }
-  block_reduce(f, s1, s2, nz);
-  uint32_t *shard_sums = partials + 3 * (size_t)MC_ARRIVAL_SHARDS * per_max;
-  if (threadIdx.x == 0) {
-    uint32_t *q = shard_sums + 3 * sh;
-    __hip_atomic_store(q + 0, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 2, nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = mc_arrive_top(tickets, gridDim.x);
-  }
-  __syncthreads();
-  if (!last) return;
-  f32_finish_chunk<true>(shard_sums, mc_arrival_nshards(gridDim.x), 0, mode, src, src_stride, dst, dst_stride,
-                         nbytes, out, seq);
-  if (threadIdx.x == 0) mc_arrivals_reset(tickets);
+  unsigned long long *w = reinterpret_cast<unsigned long long *>(tickets + MC_ARRIVAL_LINE * sh);
+  const unsigned long long old = atomicAdd(w, f32_pack(s1, s2, nz != 0));
+  if ((old & 0xffu) + 1u != mc_arrival_per(sh, gridDim.x)) return;
+  *w = 0;  // every arrival of this shard is in
+  const uint32_t t1 = mod_m(((old >> 8) & 0xffffffu) + s1), t2 = mod_m(((old >> 32) & 0xffffffu) + s2);
+  const bool tz = (old >> 56) != 0 || nz != 0;
+  unsigned long long *t = reinterpret_cast<unsigned long long *>(tickets + MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS);
+  const unsigned long long top = atomicAdd(t, f32_pack(t1, t2, tz));
+  if ((top & 0xffu) + 1u != mc_arrival_nshards(gridDim.x)) return;
+  *t = 0;
+  const uint32_t a = mod_m(((top >> 8) & 0xffffffu) + t1), b = mod_m(((top >> 32) & 0xffffffu) + t2);
+  const bool z = (top >> 56) != 0 || tz;
+  f32_write_result(final_sum(a, b, z ? 1u : 0u), 0, mode, src, src_stride, dst, dst_stride, nbytes, out, seq);
 }
 
 template <bool SC1>
@@ -318,17 +324,7 @@ MC_DEV void f32_finish_chunk(const uint32_t *partials, unsigned nslices, size_t 
   uint32_t a, b, z;
   block_reduce(p, a, b, z);
   if (threadIdx.x != 0) return;
-  const uint32_t f = final_sum(a, b, z);
-  if (mode == F_SUM) {
-    out[c] = f;
-  } else if (mode == F_FOOTER) {
-    store_le32(dst + c * dst_stride + nbytes, f);
-    if (out) out[c] = f;
-  } else {
-    out[2 * c] = f;
-    out[2 * c + 1] = load_le32(src + c * src_stride + nbytes);
-    mc_publish_verdict_seq(out, seq);
-  }
+  f32_write_result(final_sum(a, b, z), c, mode, src, src_stride, dst, dst_stride, nbytes, out, seq);
 }
 
 // one workgroup per chunk: the 256 threads fold the chunk's slices (a large
@@ -540,7 +536,8 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
   // flight); the two-level fold (64 shards) keeps the tail short
   const unsigned fg = f32_fused_grid();
   // (the fused encode keeps one slice per block, as the two-launch copy does)
-  const unsigned grid = tickets && !dst ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
+  unsigned grid = tickets && !dst ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
+  if (tickets && grid > F32_MAX_FUSED_GRID) grid = F32_MAX_FUSED_GRID;  // packed arrival fields
 #define MC_F32_U(CP, AL, U)                                                                   \
   do {                                                                                         \
     if (f32_ntld())                                                                            \
@@ -638,7 +635,7 @@ int mc_fletcher32_encode(const void *src, void *dst, size_t nbytes, void *worksp
 int mc_fletcher32_encode_fused(const void *src, void *dst, size_t nbytes, void *workspace, size_t workspace_bytes,
                                uint32_t *ticket, mc_stream_t stream) {
   if (!ticket) return mc_fletcher32_encode(src, dst, nbytes, workspace, workspace_bytes, stream);
-  if (!src || !dst || nbytes == 0 || (uintptr_t)ticket % 4) return MC_EINVAL;
+  if (!src || !dst || nbytes == 0 || (uintptr_t)ticket % 8) return MC_EINVAL;
   return f32_run(static_cast<const uint8_t *>(src), 0, static_cast<uint8_t *>(dst), 0, 1, nbytes, F_FOOTER, nullptr,
                  workspace, workspace_bytes, (hipStream_t)stream, ticket, 0);
 }
@@ -658,7 +655,7 @@ int mc_fletcher32_verify_fused(const void *src, size_t nbytes, uint32_t *out_rec
     if (seq) return MC_EINVAL;  // the two-launch path publishes no sequence word
     return mc_fletcher32_verify(src, nbytes, out_rec, workspace, workspace_bytes, stream);
   }
-  if ((uintptr_t)ticket % 4) return MC_EINVAL;
+  if ((uintptr_t)ticket % 8) return MC_EINVAL;
   if (!src || !out_rec || nbytes < 4) return MC_EINVAL;
   return f32_run(static_cast<const uint8_t *>(src), 0, nullptr, 0, 1, nbytes - 4, F_VERIFY, out_rec, workspace,
                  workspace_bytes, (hipStream_t)stream, ticket, seq);
