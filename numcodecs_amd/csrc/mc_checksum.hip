@@ -293,15 +293,23 @@ MC_DEV void ck_finish_chunk(const CrcFin &fin, const uint32_t *partials, size_t 
     }
     __syncthreads();
     uint32_t acc = 0;
-    for (size_t j0 = lo; j0 < hi; j0 += CK_FOLD_BATCH) {
-      uint32_t v[CK_FOLD_BATCH];
+    if constexpr (SC1) {  // the one-launch finish: agent-scope loads, batched
+      for (size_t j0 = lo; j0 < hi; j0 += CK_FOLD_BATCH) {
+        uint32_t v[CK_FOLD_BATCH];
 #pragma unroll
-      for (int u = 0; u < CK_FOLD_BATCH; ++u)
-        v[u] = ck_ld<SC1>(&partials[c * tiles_per_chunk + (j0 + u < hi ? j0 + u : hi - 1)]);
+        for (int u = 0; u < CK_FOLD_BATCH; ++u)
+          v[u] = ck_ld<SC1>(&partials[c * tiles_per_chunk + (j0 + u < hi ? j0 + u : hi - 1)]);
 #pragma unroll
-      for (int u = 0; u < CK_FOLD_BATCH; ++u)
-        if (j0 + u < hi)
-          acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^ v[u];
+        for (int u = 0; u < CK_FOLD_BATCH; ++u)
+          if (j0 + u < hi)
+            acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
+                  v[u];
+      }
+    } else {  // the finalize kernel: plain loads pipeline by themselves (batching measured 7.2 -> 10.5 us)
+#pragma unroll 4
+      for (size_t j = lo; j < hi; ++j)
+        acc = (T[0][acc & 0xffu] ^ T[1][(acc >> 8) & 0xffu] ^ T[2][(acc >> 16) & 0xffu] ^ T[3][acc >> 24]) ^
+              partials[c * tiles_per_chunk + j];
     }
     if (hi > lo) acc = gf_mul(acc, fin.tail[threadIdx.x], crc_poly<KIND>());
     acc = wave_xor(acc);
@@ -654,16 +662,20 @@ inline int ck_kcopy() {
   }();
   return k;
 }
-inline unsigned ck_grid_cap(bool copy) {
-  static const unsigned g = [] {
-    const int e = ck_env("MCODEC_CK_GRID", 2048);
-    return e > 0 ? (unsigned)e : 2048u;
-  }();
+// persistent-grid caps (MCODEC_CK_GRID / MCODEC_CK_GRID_COPY override).  The
+// checksum-only CRC kernels run fastest with one tile per workgroup (no
+// cap): one 256 MiB CRC32 verify 69.3 us at 2048 workgroups, 64.7 at 4096,
+// 63.9 at 8192 = every tile; Adler32 is best at 2048 (48.3 us, 50.1 at
+// 4096-8192) (tools/probe_adler_verify.py, profiles/r02/probe_ck_verify_grid.jsonl)
+inline unsigned ck_grid_cap(bool copy, bool crc) {
+  static const int g = ck_env("MCODEC_CK_GRID", 0);
   static const unsigned gc = [] {
     const int e = ck_env("MCODEC_CK_GRID_COPY", 1024);
     return e > 0 ? (unsigned)e : 1024u;
   }();
-  return copy ? gc : g;
+  if (copy) return gc;
+  if (g > 0) return (unsigned)g;
+  return crc ? 0xffffffffu : 2048u;
 }
 
 // tile size (in STEP units) for a chunk: K = 1 below 64 KiB
@@ -687,7 +699,7 @@ inline int align_class(const void *p, size_t stride, size_t nchunks) {
 template <int KIND, int K, bool COPY, int ALS, int ALD>
 void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
                   size_t total, uint32_t *parts, const CrcFin &fin, const CkFinish *fx, hipStream_t st) {
-  const unsigned cap = ck_grid_cap(COPY);
+  const unsigned cap = ck_grid_cap(COPY, KIND != K_ADLER);
   const unsigned grid = (unsigned)(total < cap ? total : cap);
   if (fx) {  // one chunk: the last block finishes it in this launch (verify, or encode with its copy)
     const unsigned fg = KIND == K_ADLER && grid > ADLER_MAX_GRID ? ADLER_MAX_GRID : grid;
