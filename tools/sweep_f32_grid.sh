@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 out=gpurun_out/sweep_f32_knobs.jsonl
-for cfg in "2048 1 4 32" "2048 0 4 32" "2048 1 8 32" "2048 0 8 32" "8192 0 4 32" "1024 0 8 64" "4096 0 8 16" "2048 0 1 32"; do
+for cfg in "2048 1 4 32" "2048 0 4 32" "2048 1 8 32" "4096 1 4 32" "4096 1 8 32" "8192 1 4 32" "8192 1 8 32" "1024 1 8 64"; do
   set -- $cfg
   echo "{\"grid\": $1, \"ntld\": $2, \"unroll\": $3, \"slice_kb\": $4}" >> $out
   MCODEC_F32_FUSED_GRID=$1 MCODEC_F32_NTLD=$2 MCODEC_F32_UNROLL=$3 MCODEC_F32_SLICE_KB=$4 \
