@@ -491,12 +491,14 @@ static int f32_env(const char *name, int def) {
   const char *e = getenv(name);
   return e ? atoi(e) : def;
 }
-static int f32_unroll() {
-  static const int u = [] {
-    const int e = f32_env("MCODEC_F32_UNROLL", 4);
-    return e == 1 || e == 8 ? e : 4;
-  }();
-  return u;
+// The one-launch single-chunk verify (no copy) defaults to 8 vectors in
+// flight and a 4096-block grid: 256 MiB verify kernel 44.1-44.3 us at
+// (2048, 4) -> 43.0 us at (4096, 8), interleaved A/B on MI355X; the copying
+// and batched passes keep 4 (profiles/r01/fletcher32_knobs_ab.jsonl).
+static int f32_unroll(bool fused_verify = false) {
+  static const int e = f32_env("MCODEC_F32_UNROLL", 0);
+  if (e == 1 || e == 4 || e == 8) return e;
+  return fused_verify ? 8 : 4;
 }
 static bool f32_ntld() {
   static const bool b = f32_env("MCODEC_F32_NTLD", 1) != 0;
@@ -505,8 +507,8 @@ static bool f32_ntld() {
 // MCODEC_F32_FUSED_GRID: block cap of the one-launch verify (256 .. 65536)
 static unsigned f32_fused_grid() {
   static const unsigned g = [] {
-    const int e = f32_env("MCODEC_F32_FUSED_GRID", 2048);
-    return (unsigned)(e >= 256 && e <= 65536 ? e : 2048);
+    const int e = f32_env("MCODEC_F32_FUSED_GRID", 4096);
+    return (unsigned)(e >= 256 && e <= 65536 ? e : 4096);
   }();
   return g;
 }
@@ -533,8 +535,9 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
   }
   // fused (one chunk): at most f32_fused_grid() blocks, each summing
   // nsl / grid slices (loads only, so a looping block keeps its loads in
-  // flight); the two-level fold (64 shards) keeps the tail short
+  // flight); the packed arrival (64 shards) keeps the tail short
   const unsigned fg = f32_fused_grid();
+  const int unroll = f32_unroll(tickets && !dst);
   // (the fused encode keeps one slice per block, as the two-launch copy does)
   unsigned grid = tickets && !dst ? (nsl < fg ? nsl : fg) : (unsigned)(nchunks * nsl);
   if (tickets && grid > F32_MAX_FUSED_GRID) grid = F32_MAX_FUSED_GRID;  // packed arrival fields
@@ -551,8 +554,8 @@ static void launch_partial(const uint8_t *src, size_t src_stride, uint8_t *dst, 
   } while (0)
 #define MC_F32_LAUNCH(CP, AL)                                                                 \
   do {                                                                                         \
-    if (f32_unroll() == 8) MC_F32_U(CP, AL, 8);                                                \
-    else if (f32_unroll() == 4) MC_F32_U(CP, AL, 4);                                           \
+    if (unroll == 8) MC_F32_U(CP, AL, 8);                                                          \
+    else if (unroll == 4) MC_F32_U(CP, AL, 4);                                                     \
     else MC_F32_U(CP, AL, 1);                                                                  \
   } while (0)
   if (dst) {
