@@ -6,7 +6,12 @@ chunks (Shuffle, BitRound)", quoted on configs[1]: Shuffle(elementsize=4) on
 a 256 MiB float32 chunk per GPU.  One step = Shuffle(4).encode +
 Shuffle(4).decode of one chunk (4 rotating buffer sets per GPU so that the
 256 MiB Infinity Cache cannot serve a step from the previous one).
-value = (bytes into encode + bytes into decode) over all ranks / time.
+value = (bytes into encode + bytes into decode) over all ranks / time of the
+slowest rank -- the whole-job aggregate the driver contract asks for; the line
+also carries per_gpu_GiBps (= value / physical GPUs, the metric's "per GPU"),
+aggregate_GiBps, frac_of_n_peak (HBM reads + writes / (physical GPUs x
+8 TB/s)), `ranks` (rank, local rank, host, pid, device, PCI location, UUID,
+elapsed) and `rehearsal` (true when ranks share a physical GPU).
 
     python bench.py [--gpus N --steps K --warmup W] [--no-cpu] [--quick]
 
@@ -32,7 +37,8 @@ Printed (rank 0): ONE JSON line with the contract's keys plus
                 processes (the same restatement);
   c5_sharded    configs[4]: 8192 x 1 MiB chunks, Shuffle(4) + Fletcher32,
                 split over the N ranks by contiguous chunk ranges (strong
-                scaling), frac of N x 8 TB/s.
+                scaling), frac of N x 8 TB/s; the timed decode includes the
+                per-step checksum verdict (device compare + one readback).
 """
 
 from __future__ import annotations
@@ -68,19 +74,44 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpu_count() -> "tuple[int, str]":
+    """GPUs a child rank will see, counted WITHOUT any HIP or torch.cuda call
+    in this process (the launcher parent must not initialise the GPU before it
+    starts the ranks).  The visibility variables win (HIP_VISIBLE_DEVICES
+    indexes into ROCR_VISIBLE_DEVICES' set, so the first one set decides);
+    otherwise the KFD topology: every node with a nonzero gfx_target_version
+    is a GPU.  Returns (count, source)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip():
+            return len([x for x in v.split(",") if x.strip()]), var
+    n = 0
+    for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(p) as f:
+                for line in f:
+                    key, _, val = line.partition(" ")
+                    if key == "gfx_target_version" and int(val) != 0:
+                        n += 1
+        except (OSError, ValueError):
+            continue
+    return n, "/sys/class/kfd/kfd/topology"
+
+
 def launch_ranks(n: int, dry_run: bool) -> int:
     """Start n rank processes of this script (one per GPU) and wait for them.
 
-    Runs in the parent before it touches the GPU (counting devices does not
-    initialise it on this image); children get RANK / LOCAL_RANK /
-    WORLD_SIZE / MASTER_* as torch.distributed.run would set them.  If a rank
-    fails, the others are stopped (they would wait at a barrier forever)."""
+    Runs in the parent, which never touches the GPU: devices are counted from
+    the visibility variables / KFD topology (visible_gpu_count), not through
+    torch.cuda or HIP.  Children get RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    as torch.distributed.run would set them.  If a rank fails, the others are
+    stopped (they would wait at a barrier forever)."""
     gloo = dry_run or os.environ.get("MCODEC_BENCH_BACKEND") == "gloo"
     if not gloo:
-        ndev = torch.cuda.device_count()
+        ndev, src = visible_gpu_count()
         if ndev < n:
-            raise SystemExit(f"bench.py --gpus {n}: only {ndev} GPU(s) visible "
-                             "(MCODEC_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
+            raise SystemExit(f"bench.py --gpus {n}: only {ndev} GPU(s) visible (counted from {src}; "
+                             "MCODEC_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
     port = _free_port()
     procs = []
     for r in range(n):
@@ -142,31 +173,85 @@ def max_over_ranks(dist, value: float) -> float:
     return float(t.item())
 
 
+def rank_identity(rank: int, local: int, dev) -> dict:
+    """Who this rank is and which physical device it drives: the PCI location
+    and UUID of the GPU (or "cpu" in a --dry-run rehearsal)."""
+    d = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "pid": os.getpid()}
+    if dev is None:
+        d.update(device="cpu", pci="cpu")
+    else:
+        p = torch.cuda.get_device_properties(dev)
+        d.update(device=f"cuda:{dev.index}", name=p.name,
+                 pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                 uuid=str(getattr(p, "uuid", "")))
+    return d
+
+
+def gather_ranks(dist, mine: dict) -> list:
+    if dist is None:
+        return [mine]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def scaling_fields(ranks: list, alg_bytes_per_rank: float, counted_bytes_per_rank: float, t_max: float,
+                   on_gpu: bool) -> dict:
+    """The N-GPU record of one timed workload (north_star: "throughput at
+    1/2/4/8 GPUs as absolute GiB/s and as fraction of the aggregate HBM
+    roofline").  `counted_bytes_per_rank` are the metric's bytes (bytes into
+    encode + decode), `alg_bytes_per_rank` the HBM algorithmic bytes (read +
+    write of every launch) each rank moved in the timed region; `t_max` is the
+    slowest rank's elapsed time.  Distinct (host, PCI location) pairs are the
+    physical GPUs: ranks sharing one (a gloo rehearsal on a one-GPU box) or a
+    CPU --dry-run are labelled `rehearsal`, and the roofline is N_physical x
+    8 TB/s."""
+    world = len(ranks)
+    phys = len({(r["host"], r["pci"]) for r in ranks}) if on_gpu else 0
+    agg = world * counted_bytes_per_rank / GiB / t_max
+    return {
+        "aggregate_GiBps": round(agg, 2),
+        "per_gpu_GiBps": round(agg / phys, 2) if phys else None,
+        "per_rank_GiBps": round(agg / world, 2),
+        "n_ranks": world,
+        "physical_gpus": phys,
+        "rehearsal": (not on_gpu) or phys < world,
+        "frac_of_n_peak": round(world * alg_bytes_per_rank / t_max / 1e9 / (phys * PEAK_GBPS), 4) if phys else None,
+        "ranks": ranks,
+    }
+
+
 def dry_run(dist, rank: int, world: int, nchunks: int) -> None:
-    """CPU rehearsal of the sharded C5 run (tests/test_distributed.py): every
-    rank takes its contiguous chunk range and encodes + verify-decodes a
-    sample of its chunks with the oracle; rank 0 prints the ranges, pids and
-    coverage.  No GPU is touched."""
+    """CPU rehearsal of the sharded run (tests/test_distributed.py): every
+    rank takes its contiguous C5 chunk range and encodes + verify-decodes a
+    sample of its chunks with the oracle, timed between barriers like the GPU
+    run; rank 0 prints the same rank / scaling record the GPU line carries,
+    labelled a rehearsal.  No GPU is touched."""
     from numcodecs_amd import shard
     from oracle import nporacle as npo
 
     lo, hi = shard.chunk_range(nchunks, rank, world)
+    sample = sorted({lo, (lo + hi) // 2, hi - 1}) if hi > lo else []
+    barrier(dist)
+    t0 = time.perf_counter()
     ok = True
-    for c in sorted({lo, (lo + hi) // 2, hi - 1}) if hi > lo else []:
+    for c in sample:
         x = np.random.default_rng(1000 + c).integers(0, 256, 4096, dtype=np.uint8)
         enc = npo.fletcher32_encode(npo.shuffle(x, 4))
         ok &= np.array_equal(npo.unshuffle(npo.fletcher32_decode(enc), 4), x)
-    info = [None] * world if dist is not None else None
-    mine = {"rank": rank, "pid": os.getpid(), "range": [lo, hi], "ok": bool(ok)}
-    if dist is not None:
-        dist.all_gather_object(info, mine)
-    else:
-        info = [mine]
+    elapsed = time.perf_counter() - t0
+    barrier(dist)
+    mine = rank_identity(rank, rank, None)
+    mine.update(range=[lo, hi], ok=bool(ok), elapsed_s=elapsed)
+    info = gather_ranks(dist, mine)
     t = max_over_ranks(dist, float(rank))
+    t_max = max(i["elapsed_s"] for i in info) or 1e-9
     if rank == 0:
         covered = sorted(c for i in info for c in range(*i["range"]))
-        print(json.dumps({"dry_run": True, "n_ranks": world, "ranks": info, "max_over_ranks": t,
-                          "chunks": nchunks, "covered_all": covered == list(range(nchunks))}), flush=True)
+        line = {"dry_run": True, "max_over_ranks": t, "chunks": nchunks,
+                "covered_all": covered == list(range(nchunks))}
+        line.update(scaling_fields(info, 2 * 2 * 4096 * 3, 2 * 4096 * 3, t_max, on_gpu=False))
+        print(json.dumps(line), flush=True)
 
 
 # ---------------------------------------------------------------------------
@@ -272,8 +357,12 @@ def run_step_timing(args, dev, dist, rank):
 def run_c5_sharded(steps, warmup, nchunks, dev, dist, rank, world):
     """configs[4]: nchunks x 1 MiB fp32 chunks, Shuffle(4) + Fletcher32 fused,
     split over ranks by contiguous chunk ranges (shard.chunk_range, no
-    collective); one step = encode + verified decode of the rank's chunks.
-    Returns (elapsed_s over all ranks, mean launch ms, local chunks)."""
+    collective); one step = encode + verified decode of the rank's chunks:
+    the decode's per-chunk (computed, stored) checksum pairs are compared on
+    the device and the verdict is read back to the host (one readback per
+    step, raising the reference's RuntimeError on a mismatch) INSIDE the
+    timed region.  Returns (this rank's elapsed_s, mean launch ms, local
+    chunks)."""
     from numcodecs_amd import batch, shard
 
     lo, hi = shard.chunk_range(nchunks, rank, world)
@@ -287,7 +376,7 @@ def run_c5_sharded(steps, warmup, nchunks, dev, dist, rank, world):
 
     def step():
         batch.shuffle_fletcher32_encode_chunks(x, 4, out=enc)
-        batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=False)
+        batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=True)
 
     for _ in range(warmup):
         step()
@@ -305,13 +394,11 @@ def run_c5_sharded(steps, warmup, nchunks, dev, dist, rank, world):
     barrier(dist)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # the decode's checksum verdicts after timing: every chunk must match
-    batch.fletcher32_unshuffle_decode_chunks(enc, MiB, 4, out=dec, check_sums=True)
     assert torch.equal(dec.view(torch.float32), x), "C5 round trip failed after timing"
     launch_ms = ev0.elapsed_time(ev1) / (2 * steps)
     del x, enc, dec
     torch.cuda.empty_cache()
-    return max_over_ranks(dist, elapsed), max_over_ranks(dist, launch_ms), b
+    return elapsed, launch_ms, b
 
 
 def _timed(fn, sets, reps):
@@ -411,11 +498,12 @@ def config_workloads(dev, cpu, sets: int = 4) -> dict:
     eb = batch.shuffle_fletcher32_encode_chunks(xb, 4)
     db = torch.empty((nb, MiB), dtype=torch.uint8, device=dev)
     t_e = _timed(lambda i: batch.shuffle_fletcher32_encode_chunks(xb, 4, out=eb), 1, 5)
-    t_d = _timed(lambda i: batch.fletcher32_unshuffle_decode_chunks(eb, MiB, 4, out=db, check_sums=False), 1, 5)
-    batch.fletcher32_unshuffle_decode_chunks(eb, MiB, 4, out=db, check_sums=True)
+    t_d = _timed(lambda i: batch.fletcher32_unshuffle_decode_chunks(eb, MiB, 4, out=db, check_sums=True), 1, 5)
     assert torch.equal(db.view(torch.float32), xb)
     out["cfg_C5"] = _cfg(2 * nb * MiB / GiB / (t_e + t_d), t_e, t_d, 2 * nb * (2 * MiB + 4),
-                         "k_shuffle_f32_enc / k_f32_unshuffle", cpu, "C5")
+                         "k_shuffle_f32_enc / k_f32_unshuffle", cpu, "C5",
+                         "decode = fused verify + unshuffle, the per-chunk verdict compared on the device and "
+                         "read back inside every timed call")
     del xb, eb, db
     torch.cuda.empty_cache()
     return out
@@ -518,12 +606,21 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    ident = rank_identity(rank, local, dev)
     elapsed, launch_ms = run_step_timing(args, dev, dist, rank)
     t = max_over_ranks(dist, elapsed)
     launch_ms = max_over_ranks(dist, launch_ms)
     value = world * args.steps * 2 * CHUNK / GiB / t  # bytes into encode + decode, all ranks
+    # headline: 2 x CHUNK into encode + decode per step (the metric's bytes),
+    # 4 x CHUNK of HBM reads + writes per step (the roofline's bytes)
+    head_ranks = gather_ranks(dist, dict(ident, elapsed_s=round(elapsed, 6)))
+    head_scale = scaling_fields(head_ranks, args.steps * 4 * CHUNK, args.steps * 2 * CHUNK, t, on_gpu=True)
 
-    c5_t, c5_launch_ms, c5_local = run_c5_sharded(args.c5_steps, 1, args.c5_chunks, dev, dist, rank, world)
+    c5_el, c5_launch_ms, c5_local = run_c5_sharded(args.c5_steps, 1, args.c5_chunks, dev, dist, rank, world)
+    c5_t = max_over_ranks(dist, c5_el)
+    c5_launch_ms = max_over_ranks(dist, c5_launch_ms)
+    c5_ranks = gather_ranks(dist, {"rank": rank, "host": ident["host"], "pci": ident["pci"],
+                                   "chunks": c5_local, "elapsed_s": round(c5_el, 6)})
 
     if rank == 0:
         achieved = 2 * CHUNK / (launch_ms * 1e-3) / 1e9  # GB/s per launch
@@ -531,11 +628,20 @@ def main():
         ceiling = copy_ceiling(dev)
         c5_bytes = args.c5_steps * 2 * args.c5_chunks * MiB
         c5_alg = c5_local * (2 * MiB + 4)  # rank 0's chunks per launch: payload in + out (+ footer)
+        c5_phys = head_scale["physical_gpus"]
         result = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
+            "value_scope": ("whole-job aggregate over all ranks (the driver contract); per_gpu_GiBps = "
+                            "value / physical_gpus is the metric's per-GPU figure (equal at N = 1)"),
             "n_gpus": world,
+            "per_gpu_GiBps": head_scale["per_gpu_GiBps"],
+            "aggregate_GiBps": head_scale["aggregate_GiBps"],
+            "frac_of_n_peak": head_scale["frac_of_n_peak"],
+            "physical_gpus": c5_phys,
+            "rehearsal": head_scale["rehearsal"],
+            "ranks": head_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t / args.steps * 1e3, 4),
@@ -565,14 +671,19 @@ def main():
             },
             "c5_sharded": {
                 "GiBps": round(c5_bytes / GiB / c5_t, 1),
+                "per_gpu_GiBps": round(c5_bytes / GiB / c5_t / c5_phys, 1),
                 "n_gpus": world,
+                "physical_gpus": c5_phys,
                 "chunks": args.c5_chunks,
                 "steps": args.c5_steps,
                 "ms_per_step": round(c5_t / args.c5_steps * 1e3, 3),
                 "scaling": "strong",
-                "frac_of_n_peak": round(c5_bytes / c5_t / 1e9 * 2 / (world * PEAK_GBPS), 4),
+                "frac_of_n_peak": round(c5_bytes / c5_t / 1e9 * 2 / (c5_phys * PEAK_GBPS), 4),
                 "kernel_GBps_rank0": round(c5_alg / (c5_launch_ms * 1e-3) / 1e9, 1),
-                "workload": "configs[4]: 8192 x 1 MiB f32, Shuffle(4)+Fletcher32 enc + verified dec, chunk ranges",
+                "workload": ("configs[4]: 8192 x 1 MiB f32 split into contiguous chunk ranges; timed step = fused "
+                             "Shuffle(4)+Fletcher32 encode + fused verify+unshuffle decode with the per-chunk "
+                             "verdict compared on the device and read back (raising on a mismatch) every step"),
+                "ranks": c5_ranks,
             },
         }
         if cpu is not None:

@@ -289,11 +289,13 @@ def fletcher32_unshuffle_decode_chunks(encoded, chunk_bytes, elementsize, out=No
                 elementsize, status.data_ptr(), ws.data_ptr(), ws.numel(), _ops.stream(rows)),
                 "mc_fletcher32_unshuffle_batch")
     if check_sums and b:
-        st = status.to(torch.int64) & 0xFFFFFFFF
-        bad = (st[:, 0] != st[:, 1]).nonzero()
-        if bad.numel():
-            i = int(bad[0, 0])
-            raise _mismatch(int(st[i, 0]), int(st[i, 1]))
+        # one compare kernel, one reduction and ONE readback on the good path
+        # (int32 equality is the equality of the 32-bit sums)
+        bad = status[:, 0] != status[:, 1]
+        if bool(bad.any()):
+            i = int(bad.nonzero()[0, 0])
+            st = status[i].to(torch.int64) & 0xFFFFFFFF
+            raise _mismatch(int(st[0]), int(st[1]))
     return out, status
 
 

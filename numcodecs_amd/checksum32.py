@@ -21,6 +21,7 @@ import torch
 from . import _native, _ops
 from .abc import Codec
 from .compat import (
+    device_out,
     download,
     empty_like_bytes,
     ensure_contiguous_ndarray,
@@ -219,6 +220,7 @@ class JenkinsLookup3(Checksum32):
                 f" match the expected checksum ({found}).\n"
                 "This could be a sign that the data has been corrupted."
             )
+        out = device_out(out)
         if out is not None:
             if is_device_tensor(out):
                 return ndarray_copy(src.data[: n - 4], out)

@@ -98,8 +98,24 @@ def _device_array_as_tensor(buf) -> "torch.Tensor | None":
             return torch.from_dlpack(buf)
         return None
     if hasattr(buf, "__cuda_array_interface__"):
-        return torch.as_tensor(buf, device="cuda")
+        # no device argument: torch takes the device the pointer lives on, so
+        # an array on another GPU is viewed there, never copied
+        return torch.as_tensor(buf)
     return None
+
+
+_OWN_TYPES = (torch.Tensor, np.ndarray, bytes, bytearray, memoryview, array.array)
+
+
+def device_out(out):
+    """`out` as this module handles it: another library's device array
+    (DLPack / ``__cuda_array_interface__``) becomes a zero-copy torch view of
+    its memory, so results are written into the caller's buffer in place;
+    anything else is returned unchanged."""
+    if out is None or isinstance(out, _OWN_TYPES):
+        return out
+    dt = _device_array_as_tensor(out)
+    return out if dt is None else dt
 
 
 def is_ndarray_like(obj) -> bool:
@@ -312,6 +328,7 @@ def device_out_bytes(out, nbytes: int, like: "DBuf | torch.Tensor") -> "torch.Te
     the result through ndarray_copy, which raises the reference's errors for
     the other cases."""
     data = like.data if isinstance(like, DBuf) else like  # the input's bytes
+    out = device_out(out)
     if out is None or not is_device_tensor(out) or out.device != data.device or nbytes == 0:
         return None
     order = _tensor_order(out)
@@ -355,6 +372,10 @@ def ndarray_copy(src, dst):
     """
     if dst is None:
         return src
+    dt = device_out(dst)  # another library's device array: write into its memory
+    if dt is not dst:
+        ndarray_copy(src, dt)
+        return dst
     if is_device_tensor(dst):
         order = _tensor_order(dst)
         if order is None:

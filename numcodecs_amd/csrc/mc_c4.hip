@@ -250,19 +250,15 @@ static unsigned c4_batch_segments(size_t nchunks, size_t n) {
 // 425 us; groups of 16 Mi elements 434 / 480 (more launch pairs); 64 Mi 364 /
 // 383; 128 Mi 360 / 363 (357 / 364 split evenly); 96 Mi and 192 Mi, with a
 // short last group, 403-450.  Default 128 Mi elements, split evenly
-// (MCODEC_C4_GROUP_MI overrides).
+// (mc_sched.c4_group_mi; the lab overrides it).
 struct C4Plan {
   size_t rows;    // chunks per group (launch pair)
   unsigned nseg;  // segments per chunk
 };
 
 static size_t c4_group_elems() {
-  static const size_t g = [] {
-    const char *e = getenv("MCODEC_C4_GROUP_MI");
-    const long v = e ? atol(e) : 0;
-    return (size_t)(v > 0 ? v : 128) << 20;
-  }();
-  return g;
+  const int v = mc_sched.c4_group_mi;  // mc_sched.h
+  return (size_t)(v > 0 ? v : 128) << 20;
 }
 
 static C4Plan c4_batch_plan(size_t nchunks, size_t n) {

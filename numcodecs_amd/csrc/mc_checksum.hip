@@ -638,41 +638,28 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// Tuning knobs (read once): MCODEC_CK_K / MCODEC_CK_KCOPY = tile size in STEP
-// units for chunks of >= 64 KiB (4, 8 or 16) without / with the fused payload
-// copy, MCODEC_CK_GRID / MCODEC_CK_GRID_COPY = persistent grid caps.  Defaults
+// Schedule (mc_sched.h): ck_k / ck_kcopy = tile size in STEP units for
+// chunks of >= 64 KiB (4, 8 or 16) without / with the fused payload copy,
+// ck_grid / ck_grid_copy = persistent grid caps.  Defaults
 // from the sweep on 64 x 4 MiB: the checksum alone is best with
 // 64 KiB tiles, the copying passes (encode, decode) with 32 KiB tiles and
 // 1024 workgroups (CRC32 decode 139 -> 120 us).
-inline int ck_env(const char *name, int def) {
-  const char *v = getenv(name);
-  return v ? atoi(v) : def;
-}
 inline int ck_kbig() {
-  static const int k = [] {
-    const int e = ck_env("MCODEC_CK_K", 16);
-    return (e == 4 || e == 8 || e == 16) ? e : 16;
-  }();
-  return k;
+  const int e = mc_sched.ck_k;
+  return (e == 4 || e == 8 || e == 16) ? e : 16;
 }
 inline int ck_kcopy() {
-  static const int k = [] {
-    const int e = ck_env("MCODEC_CK_KCOPY", 8);
-    return (e == 4 || e == 8 || e == 16) ? e : 8;
-  }();
-  return k;
+  const int e = mc_sched.ck_kcopy;
+  return (e == 4 || e == 8 || e == 16) ? e : 8;
 }
-// persistent-grid caps (MCODEC_CK_GRID / MCODEC_CK_GRID_COPY override).  The
+// persistent-grid caps (ck_grid / ck_grid_copy).  The
 // checksum-only CRC kernels run fastest with one tile per workgroup (no
 // cap): one 256 MiB CRC32 verify 69.3 us at 2048 workgroups, 64.7 at 4096,
 // 63.9 at 8192 = every tile; Adler32 is best at 2048 (48.3 us, 50.1 at
 // 4096-8192) (tools/probe_adler_verify.py, profiles/r02/probe_ck_verify_grid.jsonl)
 inline unsigned ck_grid_cap(bool copy, bool crc) {
-  static const int g = ck_env("MCODEC_CK_GRID", 0);
-  static const unsigned gc = [] {
-    const int e = ck_env("MCODEC_CK_GRID_COPY", 1024);
-    return e > 0 ? (unsigned)e : 1024u;
-  }();
+  const int g = mc_sched.ck_grid;
+  const unsigned gc = mc_sched.ck_grid_copy > 0 ? (unsigned)mc_sched.ck_grid_copy : 1024u;
   if (copy) return gc;
   if (g > 0) return (unsigned)g;
   return crc ? 0xffffffffu : 2048u;

@@ -18,6 +18,7 @@
 #include <stddef.h>
 
 #include "../../include/mcodec.h"
+#include "mc_sched.h"
 
 #define MC_DEV __device__ __forceinline__
 #define MC_HD __host__ __device__ __forceinline__

@@ -62,24 +62,13 @@ inline int copy_align(const void *p, size_t stride, size_t rows) {
   return a % 16 == 0 ? 2 : a % 4 == 0 ? 1 : 0;
 }
 
-// knobs (read once): MCODEC_COPY_U = vectors per thread per tile (4 or 8),
-// MCODEC_COPY_GRID = workgroup cap (0 = one tile per workgroup).  Defaults
-// from profiles/r01/copy_knobs_ab.jsonl: 16 KiB tiles, one per workgroup,
+// schedule (mc_sched.h): copy_u = vectors per thread per tile (4 or 8),
+// copy_grid = workgroup cap (0 = one tile per workgroup).  Defaults from
+// profiles/r01/copy_knobs_ab.jsonl: 16 KiB tiles, one per workgroup,
 // 5.7-5.9 TB/s against 4.7-5.3 TB/s for hipMemcpyAsync DtoD (256 MiB, 1 GiB).
-inline int copy_env(const char *name, int def) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : def;
-}
-inline int copy_u() {
-  static const int u = copy_env("MCODEC_COPY_U", 4) == 8 ? 8 : 4;
-  return u;
-}
+inline int copy_u() { return mc_sched.copy_u == 8 ? 8 : 4; }
 inline size_t copy_grid_cap() {
-  static const size_t g = [] {
-    const int e = copy_env("MCODEC_COPY_GRID", 0);
-    return e > 0 ? (size_t)e : (size_t)0x7fffffff;
-  }();
-  return g;
+  return mc_sched.copy_grid > 0 ? (size_t)mc_sched.copy_grid : (size_t)0x7fffffff;
 }
 
 template <int AL, int U>

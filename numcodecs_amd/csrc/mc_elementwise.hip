@@ -469,14 +469,9 @@ int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, dou
   return launch_map<K_QUANTIZE>(src, dst, n, p, (hipStream_t)stream);
 }
 
-// MCODEC_DELTA_ENC_VEC=0 keeps same-width integer encodes on k_delta_enc (A/B)
-static bool delta_enc_vec_enabled() {
-  static const bool b = [] {
-    const char *e = getenv("MCODEC_DELTA_ENC_VEC");
-    return !(e && atoi(e) == 0);
-  }();
-  return b;
-}
+// mc_sched.delta_enc_vec = 0 keeps same-width integer encodes on k_delta_enc
+// (lab A/B only)
+static bool delta_enc_vec_enabled() { return mc_sched.delta_enc_vec != 0; }
 
 int mc_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype,
                     mc_stream_t stream) {

@@ -482,42 +482,29 @@ static size_t fused_partials_bytes(unsigned nslices) {
   return (per_max + 1) * MC_ARRIVAL_SHARDS * 3 * sizeof(uint32_t);
 }
 
-// knobs (read once): MCODEC_F32_UNROLL = vectors in flight per thread in
-// k_f32_partial (1, 4, 8); MCODEC_F32_NTLD = nontemporal loads (0/1);
-// MCODEC_F32_SLICE_KB = payload bytes per workgroup.  Defaults from the sweep
-// on 64 x 4 MiB rows (profiles/r01/fletcher32_knobs_ab.jsonl): 4 loads in
-// flight and 32 KiB slices take the one-pass decode from 116 to 100 us.
-static int f32_env(const char *name, int def) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : def;
-}
+// schedule (mc_sched.h): f32_unroll = vectors in flight per thread in
+// k_f32_partial (1, 4, 8); f32_ntld = nontemporal loads (0/1); f32_slice_kb
+// = payload KiB per workgroup.  Defaults from the sweep on 64 x 4 MiB rows
+// (profiles/r01/fletcher32_knobs_ab.jsonl): 4 loads in flight and 32 KiB
+// slices take the one-pass decode from 116 to 100 us.
 // The one-launch single-chunk verify (no copy) defaults to 8 vectors in
 // flight and a 4096-block grid: 256 MiB verify kernel 44.1-44.3 us at
 // (2048, 4) -> 43.0 us at (4096, 8), interleaved A/B on MI355X; the copying
 // and batched passes keep 4 (profiles/r01/fletcher32_knobs_ab.jsonl).
 static int f32_unroll(bool fused_verify = false) {
-  static const int e = f32_env("MCODEC_F32_UNROLL", 0);
+  const int e = mc_sched.f32_unroll;
   if (e == 1 || e == 4 || e == 8) return e;
   return fused_verify ? 8 : 4;
 }
-static bool f32_ntld() {
-  static const bool b = f32_env("MCODEC_F32_NTLD", 1) != 0;
-  return b;
-}
-// MCODEC_F32_FUSED_GRID: block cap of the one-launch verify (256 .. 65536)
+static bool f32_ntld() { return mc_sched.f32_ntld != 0; }
+// f32_fused_grid: block cap of the one-launch verify (256 .. 65536)
 static unsigned f32_fused_grid() {
-  static const unsigned g = [] {
-    const int e = f32_env("MCODEC_F32_FUSED_GRID", 4096);
-    return (unsigned)(e >= 256 && e <= 65536 ? e : 4096);
-  }();
-  return g;
+  const int e = mc_sched.f32_fused_grid;
+  return (unsigned)(e >= 256 && e <= 65536 ? e : 4096);
 }
 static size_t f32_slice_bytes() {
-  static const size_t b = [] {
-    const int e = f32_env("MCODEC_F32_SLICE_KB", 32);
-    return (size_t)(e >= 4 && e <= 4096 ? e : 32) * 1024;
-  }();
-  return b;
+  const int e = mc_sched.f32_slice_kb;
+  return (size_t)(e >= 4 && e <= 4096 ? e : 32) * 1024;
 }
 
 static int align_class(const void *p, size_t stride, size_t nchunks) {

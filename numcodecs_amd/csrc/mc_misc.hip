@@ -1,5 +1,15 @@
 // mc_misc.hip -- ABI version, status strings, device query.
+#include <time.h>
+
 #include "mc_common.h"
+
+// the measured defaults (mc_sched.h); nothing in the product changes them
+mc_sched_t mc_sched = {
+    /*copy_u*/ 4,         /*copy_grid*/ 0,     /*ck_k*/ 16,           /*ck_kcopy*/ 8,
+    /*ck_grid*/ 0,        /*ck_grid_copy*/ 1024, /*f32_unroll*/ 0,    /*f32_ntld*/ 1,
+    /*f32_fused_grid*/ 4096, /*f32_slice_kb*/ 32, /*c4_group_mi*/ 128, /*delta_enc_vec*/ 1,
+    /*dscan*/ 1,          /*dscan_nt*/ 2,      /*fspec*/ 1,           /*fastdiv*/ 1,
+};
 
 extern "C" {
 
@@ -37,8 +47,21 @@ void mc_verdict_free(void *rec) {
   if (rec) (void)hipHostFree(rec);
 }
 
+static inline uint64_t mc_now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+// Spin on the verdict word for at most MC_VERDICT_SPIN_NS (a lone verify of
+// 256 MiB is ~45 us, so the usual call never leaves the spin); a verify queued
+// behind a lot of earlier work blocks in hipStreamSynchronize instead of
+// holding a host core at 100 % for as long as the stream takes.
+#define MC_VERDICT_SPIN_NS 100000ull
+
 int mc_verdict_wait(const uint32_t *rec, uint32_t seq, mc_stream_t stream) {
   if (!rec || !seq) return MC_EINVAL;
+  const uint64_t t0 = mc_now_ns();
   for (unsigned i = 1;; ++i) {
     if (__atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq) return MC_OK;
     if ((i & 1023u) == 0) {  // every ~10-20 us: has the stream ended or failed?
@@ -46,6 +69,11 @@ int mc_verdict_wait(const uint32_t *rec, uint32_t seq, mc_stream_t stream) {
       if (e == hipSuccess)
         return __atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq ? MC_OK : MC_EPROTO;
       if (e != hipErrorNotReady) return mc_hip_status(e);
+      if (mc_now_ns() - t0 > MC_VERDICT_SPIN_NS) {
+        const hipError_t s = hipStreamSynchronize((hipStream_t)stream);
+        if (s != hipSuccess) return mc_hip_status(s);
+        return __atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq ? MC_OK : MC_EPROTO;
+      }
     }
     __builtin_ia32_pause();
   }

@@ -282,12 +282,8 @@ MC_DEV double mc_div_by_const(double a, double b, double rcp) {
 
 // integer numerators (|a| < 2^64) divided by a scale in [2^-500, 2^500]: the
 // quotient and the FMA residual stay normal, so mc_div_by_const is exact.
-// MCODEC_FASTDIV=0 forces IEEE division (A/B and tests).
+// mc_sched.fastdiv = 0 forces IEEE division (lab A/B and tests).
 static inline bool mc_fastdiv_ok(double scale) {
-  static const bool enabled = [] {
-    const char *e = getenv("MCODEC_FASTDIV");
-    return !(e && atoi(e) == 0);
-  }();
   const double m = scale < 0 ? -scale : scale;
-  return enabled && m >= 0x1p-500 && m <= 0x1p500;
+  return mc_sched.fastdiv != 0 && m >= 0x1p-500 && m <= 0x1p500;
 }

@@ -908,30 +908,21 @@ static void launch_dscan_g(const uint8_t *s, uint8_t *d, size_t n, uint32_t *ws,
   const size_t ntiles = (n + ds_tile<ES>() - 1) / ds_tile<ES>();
   const unsigned gt = ds_group_tiles(ntiles);
   const unsigned rg = (unsigned)((ntiles + DS_GROUP - 1) / DS_GROUP);
-  // load policy per pass, MCODEC_DSCAN_NT (A/B): bit 0 = nontemporal loads in
+  // load policy per pass, mc_sched.dscan_nt (lab A/B): bit 0 = nontemporal loads in
   // the reduce pass, bit 1 in the apply pass.  Default 2: the reduce pass
   // keeps default-policy loads (what the Infinity Cache retains serves the
   // re-read; nt there: 256 MiB i1 / i2 / i4 decode 137 / 127 / 122 ->
   // 150 / 138 / 131 us), the apply pass reads nontemporally (132 / 127 / 120
   // us; tools/probe_dscan_nt.py, profiles/r02/probe_dscan_nt.json)
-  static const int ntm = [] {
-    const char *e = getenv("MCODEC_DSCAN_NT");
-    return e ? atoi(e) : 2;
-  }();
+  const int ntm = mc_sched.dscan_nt;  // mc_sched.h
   if (ntm & 1) k_dscan_reduce_g<ES, true><<<rg, MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles, gt);
   else k_dscan_reduce_g<ES, false><<<rg, MC_BLOCK, 0, st>>>(s, n, ws, ticket, ntiles, gt);
   if (ntm & 2) k_dscan_apply_g<ES, true><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
   else k_dscan_apply_g<ES, false><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, ws, ntiles, gt);
 }
 
-// MCODEC_DSCAN=0 selects the generic three-pass kernels (A/B)
-static bool dscan_enabled() {
-  static const bool b = [] {
-    const char *e = getenv("MCODEC_DSCAN");
-    return !(e && atoi(e) == 0);
-  }();
-  return b;
-}
+// mc_sched.dscan = 0 selects the generic three-pass kernels (lab A/B only)
+static bool dscan_enabled() { return mc_sched.dscan != 0; }
 
 template <int ES>
 static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, hipStream_t st) {
@@ -1314,14 +1305,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
   if (threadIdx.x == 0) fail[blockIdx.x] = n;
 }
 
-// MCODEC_FSPEC=0 disables the speculative float path (A/B: serial only)
-static bool fspec_enabled() {
-  static const bool b = [] {
-    const char *e = getenv("MCODEC_FSPEC");
-    return !(e && atoi(e) == 0);
-  }();
-  return b;
-}
+// mc_sched.fspec = 0 disables the speculative float path (lab A/B: serial only)
+static bool fspec_enabled() { return mc_sched.fspec != 0; }
 
 static size_t fspec_ntiles(size_t n, int dt) {
   const size_t te = fs_tile_of(dt);

@@ -12,6 +12,7 @@ import torch
 from . import _ops
 from .abc import Codec
 from .compat import (
+    device_out,
     download,
     empty_like_bytes,
     ensure_contiguous_ndarray,
@@ -65,6 +66,7 @@ class Fletcher32(Codec):
         if val != found:
             raise _mismatch(val, found)
         payload = src.data[: nbytes - FOOTER_LENGTH]
+        out = device_out(out)
         if out is not None:
             if is_device_tensor(out):
                 out_flat = ensure_contiguous_ndarray(out)
@@ -84,6 +86,7 @@ class Fletcher32(Codec):
             o[: payload.numel()] = download(payload)
             return out
         if src.host:
-            # the reference returns a zero-copy view of the input
-            return ensure_contiguous_ndarray(buf).view("uint8")[:-FOOTER_LENGTH]
+            # the reference returns a zero-copy memoryview slice of the input
+            # (`b_mv[:-FOOTER_LENGTH]`, fletcher32.pyx:113-114)
+            return memoryview(ensure_contiguous_ndarray(buf).view("uint8")[:-FOOTER_LENGTH])
         return payload

@@ -11,6 +11,7 @@ from . import _ops
 from .abc import Codec
 from .compat import (
     _TORCH_TO_NP,
+    device_out,
     empty_like_bytes,
     ensure_contiguous_ndarray,
     finish,
@@ -40,6 +41,7 @@ class Shuffle(Codec):
         res = self._run_device(buf, out, encode)
         if res is not None:
             return res
+        out = device_out(out)
         src = to_dbuf(buf)  # ensure_contiguous_ndarray semantics (shuffle.py:24)
         nbytes = src.nbytes
         es = self.elementsize

@@ -1,8 +1,11 @@
 #!/usr/bin/env bash
 # Compile the reference's own hot-path Cython extensions, from the sources
-# where they lie under /root/reference, into oracle/_ref/ (git-ignored; it
-# travels to the GPU box with the snapshot).  Test infrastructure only: used to
-# pin the oracle restatement and as bench.py's cpu_baseline "reference" leg.
+# where they lie under /root/reference, into oracle/_ref/ (git-ignored, and
+# listed in .gpurunignore: it stays in this container and never reaches the GPU
+# box).  Test infrastructure only: it pins the oracle restatement
+# (tests/test_oracle.py), generates tests/golden/, and times the reference
+# beside the restatement (tools/cpu_port_vs_ref.py).  bench.py's cpu_baseline
+# times the restatement (oracle/ncoracle.c, kind "port"), not this build.
 #
 #   src/numcodecs/_shuffle.pyx    -> oracle/_ref/_shuffle.*.so   (_doShuffle/_doUnshuffle)
 #   src/numcodecs/fletcher32.pyx  -> oracle/_ref/fletcher32.*.so (+ _utils.pxd)

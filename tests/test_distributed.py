@@ -92,6 +92,52 @@ def test_bench_self_launches_ranks_dry_run():
     assert [x["range"] for x in d["ranks"]] == [[0, 4096], [4096, 8192]]
     assert len({x["pid"] for x in d["ranks"]}) == 2 and os.getpid() not in {x["pid"] for x in d["ranks"]}
     assert all(x["ok"] for x in d["ranks"]) and d["max_over_ranks"] == 1.0
+    # the N-GPU record the GPU line carries, labelled as a rehearsal
+    assert [x["rank"] for x in d["ranks"]] == [0, 1]
+    assert all(x["device"] == "cpu" and x["elapsed_s"] > 0 for x in d["ranks"])
+    assert d["rehearsal"] is True and d["physical_gpus"] == 0
+    assert d["per_gpu_GiBps"] is None and d["frac_of_n_peak"] is None
+    assert d["aggregate_GiBps"] > 0 and abs(d["per_rank_GiBps"] * 2 - d["aggregate_GiBps"]) < 0.02
+
+
+def test_scaling_fields_physical_gpus():
+    """frac_of_n_peak divides by the PHYSICAL GPUs; ranks sharing one device
+    are a rehearsal."""
+    import bench
+
+    GiB = 1 << 30
+    mk = lambda r, pci: {"rank": r, "host": "h", "pci": pci}  # noqa: E731
+    four = [mk(r, f"0000:{r:02x}:00") for r in range(4)]
+    f = bench.scaling_fields(four, 8e12, 4 * GiB, 1.0, on_gpu=True)
+    assert f["physical_gpus"] == 4 and f["rehearsal"] is False
+    assert f["aggregate_GiBps"] == 16.0 and f["per_gpu_GiBps"] == 4.0 and f["per_rank_GiBps"] == 4.0
+    assert f["frac_of_n_peak"] == 1.0  # 4 x 8e12 B in 1 s over 4 x 8 TB/s
+    shared = [mk(r, "0000:03:00") for r in range(2)]
+    g = bench.scaling_fields(shared, 8e12, GiB, 2.0, on_gpu=True)
+    assert g["physical_gpus"] == 1 and g["rehearsal"] is True
+    assert g["aggregate_GiBps"] == 1.0 and g["per_gpu_GiBps"] == 1.0 and g["frac_of_n_peak"] == 1.0
+
+
+def test_visible_gpu_count_without_hip(monkeypatch):
+    """The launcher parent counts GPUs from the visibility variables (or the
+    KFD topology), never through torch.cuda / HIP."""
+    import bench
+
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    assert bench.visible_gpu_count() == (8, "ROCR_VISIBLE_DEVICES")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,3")
+    assert bench.visible_gpu_count() == (2, "HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    n, src = bench.visible_gpu_count()
+    assert src.startswith("/sys/class/kfd") and n >= 0
+    # and the parent never asks torch.cuda
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: (_ for _ in ()).throw(AssertionError("HIP call")))
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    with pytest.raises(SystemExit, match="only 1 GPU"):
+        bench.launch_ranks(2, dry_run=False)
 
 
 def test_bench_world_size_mismatch_fails_loudly():

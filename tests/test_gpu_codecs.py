@@ -431,6 +431,20 @@ def test_fletcher32_out(device):
     assert f.decode(result, out=data) is data
 
 
+def test_fletcher32_host_decode_returns_memoryview(device):
+    """Host input, no `out`: the reference returns a memoryview slice of the
+    input without the footer (`b_mv[:-FOOTER_LENGTH]`, fletcher32.pyx:113-114),
+    not a copy -- a memoryview over the caller's own bytes."""
+    data = np.arange(100, dtype="<i4")
+    enc = bytearray(Fletcher32().encode(data))
+    dec = Fletcher32().decode(enc)
+    assert type(dec) is memoryview and dec.nbytes == data.nbytes and dec.format == "B"
+    assert bytes(dec) == data.tobytes()
+    enc[1] = 0x5A  # a write into the input shows through the returned view
+
+    assert dec[1] == 0x5A
+
+
 def test_fletcher32_device_out_sizes(device):
     """Device `out`: exact and larger buffers receive the payload; an
     undersized one raises ValueError instead of writing out of bounds (the
@@ -639,6 +653,27 @@ def test_foreign_device_arrays_are_used_in_place(device):
         assert np.array_equal(enc.cpu().numpy(), oracle.shuffle(xh, 4))
         d = Delta(dtype="<f4")
         assert np.array_equal(d.encode(obj).cpu().numpy().view("<f4"), oracle.delta_encode(xh, "<f4"))
+
+
+def test_foreign_device_arrays_as_out(device):
+    """decode(out=<another library's device array>) writes the result into
+    that array's own memory and returns it (a foreign `out` used
+    to fall into the host branch of ndarray_copy)."""
+    from numcodecs_amd import Delta, FixedScaleOffset
+
+    x = torch.randn(4096 * 3 + 5, device=device)
+    xh = x.cpu().numpy()
+    for wrap in (_DLPackDeviceArray, _CAIDeviceArray):
+        for codec in (Shuffle(4), Delta(dtype="<f4"), FixedScaleOffset(0, 10, "<f4", "<f4")):
+            enc = codec.encode(x)
+            target = torch.full_like(x, -1.0)
+            obj = wrap(target)
+            r = codec.decode(enc, out=obj)
+            assert r is obj or (isinstance(r, torch.Tensor) and r.data_ptr() == target.data_ptr())
+            expect = codec.decode(enc)
+            assert torch.equal(target, expect.view(torch.float32).reshape(-1))
+            if isinstance(codec, Shuffle):
+                assert np.array_equal(target.cpu().numpy(), xh)
 
 
 def test_checksum_decode_threadpool_same_stream(device):

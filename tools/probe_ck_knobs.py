@@ -43,7 +43,7 @@ if __name__ == "__main__":
     for rnd in range(2):
         for k in (4, 8, 16):
             for g in (512, 1024, 2048, 4096):
-                env = dict(os.environ, MCODEC_CK_KCOPY=str(k), MCODEC_CK_GRID_COPY=str(g))
+                env = dict(os.environ, MCODEC_CK_KCOPY=str(k), MCODEC_CK_GRID_COPY=str(g), NUMCODECS_AMD_LIB=os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libmcodec_lab.so"))
                 r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env,
                                    capture_output=True, text=True, timeout=120)
                 if r.returncode:

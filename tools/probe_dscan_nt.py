@@ -46,7 +46,7 @@ if __name__ == "__main__":
     out = {}
     for rep in range(2):
         for m in (0, 1, 2, 3):
-            env = dict(os.environ, MCODEC_DSCAN_NT=str(m))
+            env = dict(os.environ, MCODEC_DSCAN_NT=str(m), NUMCODECS_AMD_LIB=os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libmcodec_lab.so"))
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env, capture_output=True,
                                text=True, timeout=120)
             if r.returncode:

@@ -1,5 +1,5 @@
 """Float Delta decode of one chunk: speculative scan (default) vs the serial
-chain (MCODEC_FSPEC=0 in a child), smooth data (every add exact) and random
+chain (the lab library's fspec = 0 schedule in a child), smooth data (every add exact) and random
 data (verification fails early, serial fix-up).  Rotating buffers; prints one
 JSON line.  Usage: python tools/probe_fspec.py"""
 import json
@@ -69,7 +69,12 @@ def time_batch(dt, rows, n, kind, reps=5):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "serial":
-        os.environ["MCODEC_FSPEC"] = "0"
+        import ctypes
+
+        from numcodecs_amd import _native
+
+        # serial chain only: a lab-library schedule (the product reads no environment)
+        assert ctypes.CDLL(_native.lib_path).mc_lab_set_sched(b"fspec", 0) != -(1 << 31)
         out = {}
         for dt in ("<f4", "<f8"):
             out[f"serial_{dt}_16MiB_smooth"] = time_decode(dt, (16 << 20) // np.dtype(dt).itemsize, "smooth", reps=3)
@@ -84,7 +89,9 @@ if __name__ == "__main__":
         print(json.dumps({dt: time_decode(dt, (256 << 20) // np.dtype(dt).itemsize, "smooth") for dt in ("<f4", "<f8")}))
         sys.exit(0)
     # the serial leg runs in a child started before this process touches the GPU
-    r = subprocess.run([sys.executable, __file__, "serial"], capture_output=True, text=True, timeout=300)
+    lab = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libmcodec_lab.so")
+    r = subprocess.run([sys.executable, __file__, "serial"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, NUMCODECS_AMD_LIB=lab))
     out = json.loads(r.stdout.strip().splitlines()[-1])
     for dt in ("<f4", "<f8"):
         for mib in (16, 256):

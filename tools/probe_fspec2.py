@@ -52,7 +52,7 @@ def main():
         out[key] = {"speculative": time_decode(dt, at, nb)}
         if dt == "<f4" and at == "<f4":
             continue
-        env = dict(os.environ, MCODEC_FSPEC="0")
+        env = dict(os.environ, MCODEC_FSPEC="0", NUMCODECS_AMD_LIB=os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libmcodec_lab.so"))
         r = subprocess.run([sys.executable, __file__, dt, at, str(16 << 20)], capture_output=True, text=True,
                            env=env, timeout=300)
         out[key]["serial_16MiB"] = json.loads(r.stdout.strip().splitlines()[-1])

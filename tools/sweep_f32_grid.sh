@@ -2,6 +2,8 @@
 # One-launch Fletcher32 verify: sweep its knobs (MCODEC_F32_FUSED_GRID,
 # MCODEC_F32_NTLD, MCODEC_F32_UNROLL, MCODEC_F32_SLICE_KB) with
 # tools/probe_verify_overhead.py; one JSON line per setting.
+# the MCODEC_* schedule variables act on the lab library only (tools/lab/lab_sched.hip)
+export NUMCODECS_AMD_LIB="$(cd "$(dirname "$0")" && pwd)/_build/libmcodec_lab.so"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
