@@ -1173,6 +1173,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
                                                          uint8_t *__restrict__ dst, size_t n, int a,
                                                          const double *__restrict__ sums,
                                                          const double *__restrict__ pre_t,
+                                                         uint64_t *__restrict__ tfail,
                                                          uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
@@ -1182,14 +1183,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t tile = blockIdx.x;
   const size_t t0 = tile * fs_tile<D>();
-  // a tile at or past a recorded failure is recomputed by the serial fix-up.
-  // Each wave reads the word itself, so waves of one workgroup may disagree
-  // when another tile's atomicMin lands in between: the exited waves leave
-  // the barriers (s_barrier waits for surviving waves only) and the
-  // remaining ones compute garbage for this tile -- harmless, because the
-  // whole tile lies at or past a recorded failure, so the fix-up rewrites
-  // it, and any index these waves report is >= t0, above the minimum.
-  if (__builtin_nontemporal_load(fail) <= t0) return;
+  // every tile is verified and stored, also past an earlier failure: the
+  // walker (k_fspec_walk) re-bases at the first failing element and jumps
+  // over the tiles recorded here as verified once it is back in sync
   typename Tr::V v[FS_Q][W];
   fs_load<A_, D>(src, n, t0, a, v);
   double p[FS_Q][W];
@@ -1221,88 +1217,277 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
     const uint64_t o = __shfl_xor(first, off, 64);
     first = o < first ? o : first;
   }
-  if (lane == 0 && first != ~(uint64_t)0) atomicMin((unsigned long long *)fail, (unsigned long long)first);
+  if (lane == 0 && first != ~(uint64_t)0) {
+    atomicMin((unsigned long long *)(tfail + tile), (unsigned long long)first);
+    atomicMin((unsigned long long *)fail, (unsigned long long)first);
+  }
 }
 
-// Batched speculative float Delta decode: one workgroup per chunk walks it
-// in tiles with a running double prefix `carry` (the next tile's candidates
-// are carry + in-tile prefix, and its first element's predecessor is the
-// previous tile's last candidate), verifying every element as in
-// k_fspec_apply.  At the first tile with a failing element the workgroup
-// records the tile's start in fail[row] and stops without storing it;
-// k_scan_serial (fix-up mode, one chain per row) then finishes that row.
-// fail[row] = n when the whole row verified.
+// ---------------------------------------------------------------------------
+// The walker: re-speculation after a failure, one workgroup per chunk.
+//
+// A failing element f means the candidates after f carry the wrong running
+// error: numpy's chain rounded at or before f, so its values are no longer
+// the exact prefix sums.  The chain's state is one value, and from a TRUE
+// value y_f the same speculation works again: candidates
+// c_i = D(y_f + (p_i - p_f)) (p = the tile's double prefix) verified per
+// element exactly as above.  The walker visits a chunk's tiles in order,
+// carrying the true value at each tile boundary, and inside a tile re-bases
+// at every failing element: the smallest failing index f is fixed with one
+// add of numpy's recurrence (c_{f-1} is verified), the candidates after it
+// are recomputed from y_f, and the tile is verified again -- so the serial
+// work is one add per rounding event, not one add per element.  Measured on
+// f4 data with rounding events (tools/fspec_model.py): 2-20 re-basings per
+// 4096-element tile for noisy sines, random walks, chirps and sparse data.
+// A tile that needs more than FSW_CAP re-basings (noise-like data, ~500 per
+// tile) finishes as a serial chain over its values staged in LDS, and the
+// following tiles start serial too, trying speculation again every
+// FSW_PROBE tiles.  By induction every tile starts from the true value, so
+// the output is bit-exact for any input.
+//
+// Single chunk: after k_fspec_apply (which verifies every tile against the
+// global prefix and records each tile's first failing index) one walker
+// starts at the first failing tile.  Whenever a tile ends on the value the
+// apply pass used as the next tile's predecessor, the walker is "in sync"
+// again: the following tiles that verified at apply time are already correct
+// in dst, so it jumps to the next tile that failed there.
+// Batches (one walker per chunk): every tile is walked, carrying the true
+// value; rowfail[row] = the first index that needed a re-basing (n if none).
+// ---------------------------------------------------------------------------
+constexpr int FSW_CAP = 16;    // re-basings per tile before the serial fallback
+constexpr int FSW_PROBE = 8;   // after a serial tile, every FSW_PROBE-th tile speculates again
+constexpr int FSW_G = 16;      // serial fallback: values per 16-B LDS read group
+constexpr int FSW_NW = MC_BLOCK / 64;
+
+// The serial chain over p[j..cnt) in place (acc = the value before p[j]),
+// numpy's order: two read groups alternate so the next group's LDS reads are
+// in flight while the current group's adds run (as in k_scan_serial).  p is
+// padded by 2 groups past cnt.
+template <int D>
+MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt, typename SerAcc<D>::T acc) {
+  using T = typename SerAcc<D>::T;
+  for (; j < cnt && (j & (FSW_G - 1)); ++j) {
+    acc = ser_add<D>(acc, p[j]);
+    p[j] = acc;
+  }
+  if (j + 2 * FSW_G <= cnt) {
+    T ga[FSW_G], gb[FSW_G];
+    ser_ld<T, FSW_G>(p + j, ga);
+    for (; j + 2 * FSW_G <= cnt; j += 2 * FSW_G) {
+      ser_ld<T, FSW_G>(p + j + FSW_G, gb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < FSW_G; ++k) {
+        acc = ser_add<D>(acc, ga[k]);
+        ga[k] = acc;
+      }
+      ser_st<T, FSW_G>(p + j, ga);
+      ser_ld<T, FSW_G>(p + j + 2 * FSW_G, ga);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < FSW_G; ++k) {
+        acc = ser_add<D>(acc, gb[k]);
+        gb[k] = acc;
+      }
+      ser_st<T, FSW_G>(p + j + FSW_G, gb);
+    }
+  }
+  for (; j < cnt; ++j) {
+    acc = ser_add<D>(acc, p[j]);
+    p[j] = acc;
+  }
+  return acc;
+}
+
+MC_DEV int fsw_local(int q, int e, int W) { return q * W * MC_BLOCK + (int)threadIdx.x * W + e; }
+
+// The first tile >= from whose apply-time verification failed (ntiles if none).
+MC_DEV size_t fsw_next_failed(const uint64_t *__restrict__ tfail, size_t from, size_t ntiles, uint64_t *ldsx) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (size_t b = from; b < ntiles; b += MC_BLOCK) {
+    const size_t i = b + threadIdx.x;
+    const bool hit = i < ntiles && __builtin_nontemporal_load(tfail + i) != ~(uint64_t)0;
+    const unsigned long long bal = __ballot(hit);
+    if (lane == 0) ldsx[wave] = bal ? b + (size_t)wave * 64 + (size_t)(__ffsll(bal) - 1) : ~(uint64_t)0;
+    __syncthreads();
+    uint64_t m = ldsx[0];
+#pragma unroll
+    for (int w = 1; w < FSW_NW; ++w) m = ldsx[w] < m ? ldsx[w] : m;
+    __syncthreads();
+    if (m != ~(uint64_t)0) return (size_t)m;
+  }
+  return ntiles;
+}
+
 template <int A_, int D>
-__global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restrict__ src,
-                                                        size_t src_stride, uint8_t *__restrict__ dst,
-                                                        size_t dst_stride, size_t n, int a,
-                                                        uint64_t *__restrict__ fail) {
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restrict__ src, size_t src_stride,
+                                                        uint8_t *__restrict__ dst, size_t dst_stride, size_t n,
+                                                        int a, uint64_t *__restrict__ rowfail,
+                                                        const double *__restrict__ sums,
+                                                        const double *__restrict__ pre,
+                                                        const uint64_t *__restrict__ tfail,
+                                                        const uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
+  using V = typename Tr::V;
   constexpr int W = Tr::W;
-  __shared__ double lds[2][FS_Q][MC_BLOCK / 64];
-  __shared__ S ldsc[2][FS_Q][MC_BLOCK / 64];
-  __shared__ uint64_t ldsf[2][MC_BLOCK / 64];
-  __shared__ double ldsp[2];
+  constexpr int TE = (int)fs_tile<D>();
+  __shared__ double lds[FS_Q][FSW_NW];
+  __shared__ S ldsc[FS_Q][FSW_NW];
+  __shared__ uint64_t ldsf[FSW_NW];
+  __shared__ S ldsv[FSW_NW];
+  __shared__ double ldsp[FSW_NW];
+  __shared__ uint64_t ldsx[FSW_NW];
+  __shared__ S ldsy;
+  __shared__ __attribute__((aligned(16))) V xs[TE + 2 * FSW_G];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool single = sums != nullptr;
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
-  double carry = 0.0;
-  S prevc = (S)0;
-  int par = 0;
-  typename Tr::V nv[FS_Q][W];
-  fs_load<A_, D>(src, n, 0, a, nv);
-  for (size_t t0 = 0; t0 < n; t0 += fs_tile<D>(), par ^= 1) {
-    typename Tr::V v[FS_Q][W];
+  const size_t ntiles = (n + TE - 1) / TE;
+  size_t t = 0;
+  bool has_in = false;
+  S yin = (S)0;
+  if (single) {
+    const uint64_t f = *fail;  // the first index that failed at apply time
+    if (f >= n) return;        // everything verified: dst is final
+    t = (size_t)(f / TE);
+    has_in = t > 0;
+    if (has_in) yin = Tr::round(pre[t - 1] + sums[t - 1]);  // tile t-1 verified: its last candidate
+  }
+  uint64_t first_rebase = n;
+  int serial_run = 0;
+  V nv[FS_Q][W];
+  fs_load<A_, D>(src, n, t * TE, a, nv);
+  while (t < ntiles) {
+    const size_t t0 = t * (size_t)TE;
+    V v[FS_Q][W];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
       for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
-    if (t0 + fs_tile<D>() < n) fs_load<A_, D>(src, n, t0 + fs_tile<D>(), a, nv);  // next tile in flight
+    if (t + 1 < ntiles) fs_load<A_, D>(src, n, t0 + TE, a, nv);  // the usual successor, in flight
     double p[FS_Q][W];
-    fs_tile_scan<typename Tr::V, W>(v, p, lds[par]);
-    S c[FS_Q][W], up[FS_Q];
+    fs_tile_scan<V, W>(v, p, lds);
+    const int cnt = (int)(n - t0 < (size_t)TE ? n - t0 : (size_t)TE);
+    S c[FS_Q][W];
+    int fpos = -1;     // elements at local index <= fpos are final
+    S fixed = yin;     // the true value at fpos (the tile input while fpos < 0)
+    double bval = has_in ? (double)Tr::val(yin) : 0.0, bpre = 0.0;
+    bool go_serial = serial_run > 0 && (t % FSW_PROBE) != 0;
+    int steps = 0;
+    while (!go_serial) {
+      S up[FS_Q];
 #pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
+      for (int q = 0; q < FS_Q; ++q) {
 #pragma unroll
-      for (int e = 0; e < W; ++e) c[q][e] = Tr::round(carry + p[q][e]);
-      up[q] = Tr::shfl_up1(c[q][W - 1]);
-      if (lane == 63) ldsc[par][q][wave] = c[q][W - 1];
+        for (int e = 0; e < W; ++e) {
+          const int li = fsw_local(q, e, W);
+          if (li > fpos) c[q][e] = Tr::round(bval + (p[q][e] - bpre));
+          else if (li == fpos) c[q][e] = fixed;
+        }
+        up[q] = Tr::shfl_up1(c[q][W - 1]);
+        if (lane == 63) ldsc[q][wave] = c[q][W - 1];
+      }
+      __syncthreads();
+      uint64_t first = ~(uint64_t)0;
+      S fv = (S)0;
+      double fp = 0.0;
+#pragma unroll
+      for (int q = 0; q < FS_Q; ++q) {
+        const S p0 = lane ? up[q] : wave ? ldsc[q][wave - 1] : q ? ldsc[q - 1][FSW_NW - 1] : yin;
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+          const int li = fsw_local(q, e, W);
+          const size_t g = t0 + (size_t)li;
+          const S pv = e ? c[q][e - 1] : p0;
+          const S r = (g == 0) ? Tr::store(v[q][0]) : Tr::store(Tr::step(Tr::val(pv), v[q][e]));
+          const bool ok = Tr::bits(c[q][e]) == Tr::bits(r) && Tr::finite(c[q][e]);
+          if (li > fpos && li < cnt && !ok && first == ~(uint64_t)0) {
+            first = (uint64_t)li;
+            fv = r;
+            fp = p[q][e];
+          }
+        }
+      }
+      uint64_t m = first;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(m, off, 64);
+        m = o < m ? o : m;
+      }
+      if (lane == 0) ldsf[wave] = m;
+      if (m != ~(uint64_t)0 && first == m) {  // the owner of the wave's smallest failure
+        ldsv[wave] = fv;
+        ldsp[wave] = fp;
+      }
+      __syncthreads();
+      int wm = 0;
+#pragma unroll
+      for (int w = 1; w < FSW_NW; ++w) wm = ldsf[w] < ldsf[wm] ? w : wm;
+      const uint64_t f = ldsf[wm];
+      if (f == ~(uint64_t)0) break;  // the tile verified from the true values before it
+      if (first_rebase == n) first_rebase = t0 + f;
+      // re-base at f: numpy's value there (its predecessor is verified)
+      fpos = (int)f;
+      fixed = ldsv[wm];
+      bval = (double)Tr::val(fixed);
+      bpre = ldsp[wm];
+      if (++steps >= FSW_CAP) go_serial = true;
     }
-    __syncthreads();
-    S p0[FS_Q];
+    if (go_serial) {
+      // serial fallback: the tile's values in element order in LDS, one lane
+      // runs numpy's chain from the last true value, every lane reads back
+      if (first_rebase == n) first_rebase = t0 + (uint64_t)(fpos < 0 ? 0 : fpos);
 #pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
-      if (lane) p0[q] = up[q];
-      else if (wave) p0[q] = ldsc[par][q][wave - 1];
-      else p0[q] = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
-    }
-    uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
+      for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint64_t o = __shfl_xor(first, off, 64);
-      first = o < first ? o : first;
-    }
-    if (lane == 0) ldsf[par][wave] = first;
-    if (threadIdx.x == MC_BLOCK - 1) ldsp[par] = carry + p[FS_Q - 1][W - 1];
-    __syncthreads();
-    uint64_t tf = ldsf[par][0];
+        for (int e = 0; e < W; ++e) xs[fsw_local(q, e, W)] = v[q][e];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int j = fpos + 1;
+        V acc;
+        if (fpos >= 0) acc = Tr::val(fixed);
+        else if (has_in) acc = Tr::val(yin);
+        else {  // the chunk's first element: out[0] = enc[0]
+          acc = xs[0];
+          j = 1;
+        }
+        fsw_chain<D>(xs, j, cnt, acc);
+      }
+      __syncthreads();
 #pragma unroll
-    for (int j = 1; j < MC_BLOCK / 64; ++j) tf = ldsf[par][j] < tf ? ldsf[par][j] : tf;
-    if (tf != ~(uint64_t)0) {  // uniform across the workgroup
-      // the failing tile is not stored: the serial fix-up restarts at its
-      // first element (a chunk that fails in its first tile -- random data --
-      // then costs the serial chain alone, with no speculative stores)
-      if (threadIdx.x == 0) fail[blockIdx.x] = t0;
-      return;
+      for (int q = 0; q < FS_Q; ++q)
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+          const int li = fsw_local(q, e, W);
+          if (li > fpos) c[q][e] = Tr::store(xs[li]);
+          else if (li == fpos) c[q][e] = fixed;
+        }
+      ++serial_run;
+    } else {
+      serial_run = 0;
     }
     fs_store<A_, D>(dst, n, t0, c);
-    // next tile: prefix = this tile's last prefix (thread MC_BLOCK-1's, via
-    // LDS), predecessor = this tile's last candidate
-    carry = ldsp[par];
-    prevc = ldsc[par][FS_Q - 1][MC_BLOCK / 64 - 1];
+    if (t + 1 >= ntiles) break;
+    if (threadIdx.x == MC_BLOCK - 1) ldsy = c[FS_Q - 1][W - 1];  // the tile is full: its last element
+    __syncthreads();
+    yin = ldsy;
+    has_in = true;
+    if (single && Tr::bits(yin) == Tr::bits(Tr::round(pre[t] + sums[t]))) {
+      // in sync with the apply pass: tiles that verified there are final
+      const size_t nt = fsw_next_failed(tfail, t + 1, ntiles, ldsx);
+      if (nt >= ntiles) break;
+      if (nt != t + 1) {
+        t = nt;
+        yin = Tr::round(pre[nt - 1] + sums[nt - 1]);
+        fs_load<A_, D>(src, n, nt * (size_t)TE, a, nv);
+        continue;
+      }
+    }
+    ++t;
   }
-  if (threadIdx.x == 0) fail[blockIdx.x] = n;
+  if (!single && threadIdx.x == 0) rowfail[blockIdx.x] = first_rebase;
 }
 
 // mc_sched.fspec = 0 disables the speculative float path (lab A/B: serial only)
@@ -1322,8 +1507,9 @@ static bool fspec_types_ok(int astype, int dtype) {
          mc_float_loop_dtype(astype, dtype) == dtype;
 }
 
-// tile totals, tile prefixes, the failure word
-static size_t fspec_ws_bytes(size_t n, int dt) { return (2 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
+// tile totals, tile prefixes, per-tile first failures, the first failure
+// (the last word, read by the tests)
+static size_t fspec_ws_bytes(size_t n, int dt) { return (3 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
 
 // Tile prefixes by many workgroups (one per 256 tiles): workgroup g sums
 // all totals before its range itself (coalesced, 8 loads in flight per
@@ -1334,6 +1520,7 @@ static size_t fspec_ws_bytes(size_t n, int dt) { return (2 * fspec_ntiles(n, dt)
 // fine: the apply pass only relies on the stored pre[] and sums[].
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict__ sums,
                                                        double *__restrict__ pre, size_t ntiles,
+                                                       uint64_t *__restrict__ tfail,
                                                        uint64_t *__restrict__ fail, size_t n) {
   __shared__ double lds[2][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1365,7 +1552,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict
     base += lds[0][j];
     if (j < wave) w += lds[1][j];
   }
-  if (b + threadIdx.x < ntiles) pre[b + threadIdx.x] = base + (w + (lane ? ex : 0.0));
+  if (b + threadIdx.x < ntiles) {
+    pre[b + threadIdx.x] = base + (w + (lane ? ex : 0.0));
+    tfail[b + threadIdx.x] = ~(uint64_t)0;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) *fail = n;
 }
 
@@ -1373,11 +1563,12 @@ template <int A_, int D>
 static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st) {
   const size_t ntiles = fspec_ntiles(n, D);
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
-  uint64_t *fail = reinterpret_cast<uint64_t *>(pre + ntiles);
+  uint64_t *tfail = reinterpret_cast<uint64_t *>(pre + ntiles), *fail = tfail + ntiles;
   k_fspec_reduce<A_, D><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
-  k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, fail, n);
-  k_fspec_apply<A_, D><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, pre, fail);
-  k_scan_serial<A_, D, true, 32768, 32><<<1, 128, 0, st>>>(s, 0, d, 0, n, a, fail);
+  k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail, n);
+  k_fspec_apply<A_, D><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, pre, tfail, fail);
+  // one walker from the first failing tile (returns at once if none failed)
+  k_fspec_walk<A_, D><<<1, MC_BLOCK, 0, st>>>(s, 0, d, 0, n, a, nullptr, sums, pre, tfail, fail);
 }
 
 static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int dt, void *ws, hipStream_t st) {
@@ -1393,16 +1584,12 @@ static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int 
   }
 }
 
-// rows that failed verification finish as one serial chain each (the
-// schedules of launch_serial: small LDS slots when many chains share a CU;
-// 4 KiB slots measured no different here)
+// one walker per row (k_fspec_walk)
 template <int A_, int D>
 static void launch_fspec_rows(const uint8_t *sc, size_t src_stride, uint8_t *dc, size_t dst_stride, size_t n, int a,
                               uint64_t *fail, unsigned g, hipStream_t st) {
-  k_fspec_rows<A_, D><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
-  constexpr int GRP = D == MC_F8 ? 16 : 32;
-  if (g >= 256) k_scan_serial<A_, D, true, 8192, GRP><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
-  else k_scan_serial<A_, D, true, 32768, 32><<<g, 128, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
+  k_fspec_walk<A_, D><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr, nullptr, nullptr,
+                                            nullptr);
 }
 
 static void launch_fspec_rows_any(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a, int dt,

@@ -58,7 +58,7 @@ def _decode_raw(enc_np, dt):
     a = _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    assert ws_n == (2 * ntiles + 1) * 8
+    assert ws_n == (3 * ntiles + 1) * 8  # totals, prefixes, per-tile failures, first failure
     ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
     _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
                                               None, _ops.stream(src)), "mc_delta_decode")

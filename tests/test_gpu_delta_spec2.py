@@ -50,7 +50,7 @@ def _decode_raw(enc_np, dt, at):
     a, d = _ops.dtype_code(at), _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, d)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    assert ws_n == ((2 * ntiles + 1) * 8 if _speculative(dt, at) else 0)
+    assert ws_n == ((3 * ntiles + 1) * 8 if _speculative(dt, at) else 0)
     ws = torch.zeros(max(ws_n // 8, 1), dtype=torch.int64, device=dev)
     _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d,
                                               ws.data_ptr() if ws_n else None, ws_n, None, _ops.stream(src)),
