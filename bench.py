@@ -209,10 +209,11 @@ def scaling_fields(ranks: list, alg_bytes_per_rank: float, counted_bytes_per_ran
     world = len(ranks)
     phys = len({(r["host"], r["pci"]) for r in ranks}) if on_gpu else 0
     agg = world * counted_bytes_per_rank / GiB / t_max
+    sig = lambda x: float(f"{x:.6g}")  # noqa: E731  (6 significant digits: rehearsal rates are tiny)
     return {
-        "aggregate_GiBps": round(agg, 2),
-        "per_gpu_GiBps": round(agg / phys, 2) if phys else None,
-        "per_rank_GiBps": round(agg / world, 2),
+        "aggregate_GiBps": sig(agg),
+        "per_gpu_GiBps": sig(agg / phys) if phys else None,
+        "per_rank_GiBps": sig(agg / world),
         "n_ranks": world,
         "physical_gpus": phys,
         "rehearsal": (not on_gpu) or phys < world,

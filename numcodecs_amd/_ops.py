@@ -34,6 +34,7 @@ def dtype_code(dt) -> int:
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_capturing = getattr(torch._C, "_cuda_isCurrentStreamCapturing", None) or torch.cuda.is_current_stream_capturing
 _cur_device = getattr(torch._C, "_cuda_getDevice", None)  # the current device index
 
 
@@ -60,6 +61,7 @@ class _VerifySlot:
     def __init__(self, device):
         self.device = device
         self.ticket = torch.zeros(MC_ARRIVAL_WORDS, dtype=torch.int32, device=device)
+        self.ticket_ptr = self.ticket.data_ptr()
         self.ws = torch.empty(1 << 20, dtype=torch.uint8, device=device)
         self.rec = lib.mc_verdict_alloc()
         if not self.rec:
@@ -126,7 +128,7 @@ def arrival_ticket(t: torch.Tensor, st: int):
 
 def _verify_slot(t: torch.Tensor, st: int):
     """The stream's verify slot, or None during HIP-graph capture."""
-    if torch.cuda.is_current_stream_capturing():
+    if _capturing():
         return None
     slots = getattr(_TLS, "slots", None)
     if slots is None:
@@ -345,6 +347,33 @@ def fletcher32_verify(src, nbytes) -> "tuple[int, int]":
         check(lib.mc_fletcher32_verify(src.data_ptr(), nbytes, pair.data_ptr(), ws.data_ptr(),
                                        ws.numel(), stream(src)), "mc_fletcher32_verify")
         return _read_pair(pair)
+
+
+def fletcher32_decode_device(buf: torch.Tensor):
+    """Fletcher32.decode of a flat contiguous uint8 device tensor on the
+    current device (the Zarr case), host time kept off the GPU's critical
+    path: only what the launch needs runs before it (stream, the stream's
+    verify slot, the workspace), the payload view is made while the kernel
+    runs, and the host then waits on the verdict word.  Returns
+    (payload, computed, stored), or None for the general path (other device,
+    HIP-graph capture, too short)."""
+    n = buf.numel()
+    idx = buf.get_device()
+    if n <= 4 or _raw_stream is None or _cur_device is None or idx != _cur_device():
+        return None
+    st = _raw_stream(idx)
+    sl = _verify_slot(buf, st)
+    if sl is None:
+        return None
+    ws = sl.workspace_for(("f32", n), lambda: lib.mc_fletcher32_workspace(n))
+    seq = sl.next_seq()
+    rc = lib.mc_fletcher32_verify_fused(buf.data_ptr(), n, sl.out_ptr, seq, ws.data_ptr(), ws.numel(),
+                                        sl.ticket_ptr, st)
+    if rc:
+        check(rc, "mc_fletcher32_verify_fused")
+    payload = buf[: n - 4]  # while the kernel runs
+    val, found = sl.read(st, seq)
+    return payload, val, found
 
 
 def fletcher32(src, nbytes) -> int:

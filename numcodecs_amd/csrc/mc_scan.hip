@@ -1223,6 +1223,87 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   }
 }
 
+// Batched speculative float Delta decode: one workgroup per chunk walks it
+// in tiles with a running double prefix `carry` (the next tile's candidates
+// are carry + in-tile prefix, and its first element's predecessor is the
+// previous tile's last candidate), verifying every element as in
+// k_fspec_apply.  At the first tile with a failing element the workgroup
+// records the tile's start in fail[row] and stops without storing it; the
+// walker (k_fspec_walk, one workgroup per row) resumes that row there.
+// fail[row] = n when the whole row verified.
+template <int A_, int D>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restrict__ src,
+                                                        size_t src_stride, uint8_t *__restrict__ dst,
+                                                        size_t dst_stride, size_t n, int a,
+                                                        uint64_t *__restrict__ fail) {
+  using Tr = FsT<A_, D>;
+  using S = typename Tr::S;
+  constexpr int W = Tr::W;
+  __shared__ double lds[2][FS_Q][MC_BLOCK / 64];
+  __shared__ S ldsc[2][FS_Q][MC_BLOCK / 64];
+  __shared__ uint64_t ldsf[2][MC_BLOCK / 64];
+  __shared__ double ldsp[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  src += (size_t)blockIdx.x * src_stride;
+  dst += (size_t)blockIdx.x * dst_stride;
+  double carry = 0.0;
+  S prevc = (S)0;
+  int par = 0;
+  typename Tr::V nv[FS_Q][W];
+  fs_load<A_, D>(src, n, 0, a, nv);
+  for (size_t t0 = 0; t0 < n; t0 += fs_tile<D>(), par ^= 1) {
+    typename Tr::V v[FS_Q][W];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q)
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
+    if (t0 + fs_tile<D>() < n) fs_load<A_, D>(src, n, t0 + fs_tile<D>(), a, nv);  // next tile in flight
+    double p[FS_Q][W];
+    fs_tile_scan<typename Tr::V, W>(v, p, lds[par]);
+    S c[FS_Q][W], up[FS_Q];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+#pragma unroll
+      for (int e = 0; e < W; ++e) c[q][e] = Tr::round(carry + p[q][e]);
+      up[q] = Tr::shfl_up1(c[q][W - 1]);
+      if (lane == 63) ldsc[par][q][wave] = c[q][W - 1];
+    }
+    __syncthreads();
+    S p0[FS_Q];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      if (lane) p0[q] = up[q];
+      else if (wave) p0[q] = ldsc[par][q][wave - 1];
+      else p0[q] = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
+    }
+    uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(first, off, 64);
+      first = o < first ? o : first;
+    }
+    if (lane == 0) ldsf[par][wave] = first;
+    if (threadIdx.x == MC_BLOCK - 1) ldsp[par] = carry + p[FS_Q - 1][W - 1];
+    __syncthreads();
+    uint64_t tf = ldsf[par][0];
+#pragma unroll
+    for (int j = 1; j < MC_BLOCK / 64; ++j) tf = ldsf[par][j] < tf ? ldsf[par][j] : tf;
+    if (tf != ~(uint64_t)0) {  // uniform across the workgroup
+      // the failing tile is not stored: the serial fix-up restarts at its
+      // first element (a chunk that fails in its first tile -- random data --
+      // then costs the serial chain alone, with no speculative stores)
+      if (threadIdx.x == 0) fail[blockIdx.x] = t0;
+      return;
+    }
+    fs_store<A_, D>(dst, n, t0, c);
+    // next tile: prefix = this tile's last prefix (thread MC_BLOCK-1's, via
+    // LDS), predecessor = this tile's last candidate
+    carry = ldsp[par];
+    prevc = ldsc[par][FS_Q - 1][MC_BLOCK / 64 - 1];
+  }
+  if (threadIdx.x == 0) fail[blockIdx.x] = n;
+}
+
 // ---------------------------------------------------------------------------
 // The walker: re-speculation after a failure, one workgroup per chunk.
 //
@@ -1254,9 +1335,10 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
 // Batches (one walker per chunk): every tile is walked, carrying the true
 // value; rowfail[row] = the first index that needed a re-basing (n if none).
 // ---------------------------------------------------------------------------
-constexpr int FSW_CAP = 16;    // re-basings per tile before the serial fallback
-constexpr int FSW_PROBE = 8;   // after a serial tile, every FSW_PROBE-th tile speculates again
-constexpr int FSW_G = 16;      // serial fallback: values per 16-B LDS read group
+constexpr int FSW_CAP = 16;        // re-basings per tile before the serial fallback
+constexpr int FSW_PROBE = 8;       // after a serial tile, every FSW_PROBE-th tile speculates again ...
+constexpr int FSW_PROBE_CAP = 2;   // ... with at most this many re-basings
+constexpr int FSW_G = 32;          // serial chain: values per LDS read group (8 x 16 B in flight)
 constexpr int FSW_NW = MC_BLOCK / 64;
 
 // The serial chain over p[j..cnt) in place (acc = the value before p[j]),
@@ -1299,7 +1381,147 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
   return acc;
 }
 
-MC_DEV int fsw_local(int q, int e, int W) { return q * W * MC_BLOCK + (int)threadIdx.x * W + e; }
+// The walker's tile layout: wave w owns the contiguous quarter
+// [w*QE, (w+1)*QE) of the tile (QE = FS_Q * W * 64 elements), as FS_Q
+// segments of W*64 elements with lane l's 16-B vector at W*l: every wave
+// access is 1 KiB contiguous, and every predecessor except a quarter's first
+// element is inside the same wave (DPP shift / readlane, no LDS).
+template <int D> constexpr int fsw_qe() { return FS_Q * fs_w_of(D) * 64; }
+MC_DEV int fsw_li(int q, int e, int W) {
+  return (int)(threadIdx.x >> 6) * FS_Q * W * 64 + q * W * 64 + (int)(threadIdx.x & 63) * W + e;
+}
+
+// lane i <- lane i - 1 of the wave (DPP wave_shr:1; lane 0 gets `fill`)
+MC_DEV uint32_t fsw_shr1(uint32_t x, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x138, 0xF, 0xF, false);
+}
+template <typename S>
+MC_DEV S fsw_up1(S c) {
+  if constexpr (sizeof(S) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, c);
+    const uint64_t r = (uint64_t)fsw_shr1((uint32_t)b, 0) | ((uint64_t)fsw_shr1((uint32_t)(b >> 32), 0) << 32);
+    return __builtin_bit_cast(S, r);
+  } else if constexpr (sizeof(S) == 4) {
+    return __builtin_bit_cast(S, fsw_shr1(__builtin_bit_cast(uint32_t, c), 0));
+  } else {
+    return __builtin_bit_cast(S, (uint16_t)fsw_shr1(__builtin_bit_cast(uint16_t, c), 0));
+  }
+}
+template <typename T>
+MC_DEV T fsw_readlane(T x, int l) {  // l wave-uniform
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l) << 32);
+    return __builtin_bit_cast(T, r);
+  } else if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint32_t, x), l));
+  } else {
+    return __builtin_bit_cast(T, (uint16_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint16_t, x), l));
+  }
+}
+
+// branch-free select (bitwise, so the compiler keeps it a v_cndmask-free
+// and/or instead of sinking an expensive operand into a branch)
+template <typename T>
+MC_DEV T fsw_sel(bool cond, T a, T b) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t m = 0 - (uint64_t)cond;
+    return __builtin_bit_cast(T, (__builtin_bit_cast(uint64_t, a) & m) | (__builtin_bit_cast(uint64_t, b) & ~m));
+  } else if constexpr (sizeof(T) == 4) {
+    const uint32_t m = 0 - (uint32_t)cond;
+    return __builtin_bit_cast(T, (__builtin_bit_cast(uint32_t, a) & m) | (__builtin_bit_cast(uint32_t, b) & ~m));
+  } else {
+    const uint16_t m = (uint16_t)(0 - (uint32_t)cond);
+    return __builtin_bit_cast(T, (uint16_t)((__builtin_bit_cast(uint16_t, a) & m) |
+                                            (__builtin_bit_cast(uint16_t, b) & (uint16_t)~m)));
+  }
+}
+
+template <int A_, int D>
+MC_DEV void fsw_load(const uint8_t *src, size_t n, size_t t0, int a,
+                     typename FsT<A_, D>::V (&v)[FS_Q][FsT<A_, D>::W]) {
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
+    if constexpr (A_ == D) {
+      if (e0 + W <= n) {
+        const typename Tr::svec x =
+            __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
+#pragma unroll
+        for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e)
+          v[q][e] = e0 + e < n ? (typename Tr::V)reinterpret_cast<const typename Tr::S *>(src)[e0 + e]
+                               : (typename Tr::V)0;
+      }
+    } else {
+      const int as = mc_itemsize(a);
+      uint64_t b[W];
+#pragma unroll
+      for (int e = 0; e < W; ++e) b[e] = e0 + e < n ? mc_load_elem_u(src, e0 + e, as) : 0;
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = e0 + e < n ? Tr::from_bits(b[e], a) : (typename Tr::V)0;
+    }
+  }
+}
+
+template <int A_, int D>
+MC_DEV void fsw_store(uint8_t *dst, size_t n, size_t t0, const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W]) {
+  using Tr = FsT<A_, D>;
+  constexpr int W = Tr::W;
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
+    if (e0 + W <= n) {
+      typename Tr::svec x;
+#pragma unroll
+      for (int e = 0; e < W; ++e) x[e] = c[q][e];
+      __builtin_nontemporal_store(x, reinterpret_cast<typename Tr::svec *>(dst + e0 * sizeof(typename Tr::S)));
+    } else {
+      for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<typename Tr::S *>(dst)[e0 + e] = c[q][e];
+    }
+  }
+}
+
+// p[q][e] = the tile-relative inclusive double prefix of this thread's
+// elements in the walker layout (any fixed association: candidates only
+// propose, the per-element check decides)
+template <typename V, int W>
+MC_DEV void fsw_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double *ldsq) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double base = 0.0;
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q) {
+    p[q][0] = (double)v[q][0];
+#pragma unroll
+    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (double)v[q][e];
+    double incl = p[q][W - 1];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl = o + incl;
+    }
+    const double ex = __shfl_up(incl, 1, 64);
+    const double pre = base + (lane ? ex : 0.0);
+#pragma unroll
+    for (int e = 0; e < W; ++e) p[q][e] = pre + p[q][e];
+    base = base + fsw_readlane(incl, 63);
+  }
+  if (lane == 0) ldsq[wave] = base;  // the quarter's total
+  __syncthreads();
+  double off = 0.0;
+#pragma unroll
+  for (int w = 0; w < FSW_NW; ++w)
+    if (w < wave) off = off + ldsq[w];
+#pragma unroll
+  for (int q = 0; q < FS_Q; ++q)
+#pragma unroll
+    for (int e = 0; e < W; ++e) p[q][e] = off + p[q][e];
+}
 
 // The first tile >= from whose apply-time verification failed (ntiles if none).
 MC_DEV size_t fsw_next_failed(const uint64_t *__restrict__ tfail, size_t from, size_t ntiles, uint64_t *ldsx) {
@@ -1319,6 +1541,87 @@ MC_DEV size_t fsw_next_failed(const uint64_t *__restrict__ tfail, size_t from, s
   return ntiles;
 }
 
+// Serial streaming for noise-like stretches (tiles [tb, te)): lane 0 of
+// wave 0 runs numpy's chain over one tile's values in an LDS buffer while
+// waves 1-3 store the previous tile's results and load the next tile into the
+// other buffer (k_scan_serial's double-buffered scheme inside the walker).
+// Returns the chain's value after the last element of tile te - 1.
+template <int A_, int D>
+MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_t n, int a, size_t tb, size_t te,
+                                         typename FsT<A_, D>::S yin, bool has_in,
+                                         typename FsT<A_, D>::V (*xs)[fs_tile_of(D) + 2 * FSW_G],
+                                         typename FsT<A_, D>::S *ldsy) {
+  using Tr = FsT<A_, D>;
+  using S = typename Tr::S;
+  using V = typename Tr::V;
+  constexpr int W = Tr::W;
+  constexpr int TE = (int)fs_tile<D>();
+  constexpr int NV = TE / W;  // vectors per tile
+  const int wave = threadIdx.x >> 6;
+  auto io_load = [&](size_t t, V *buf, int from, int step) {
+    const size_t t0 = t * (size_t)TE;
+    for (int k = from; k < NV; k += step) {
+      const size_t e0 = t0 + (size_t)k * W;
+      if constexpr (A_ == D) {
+        if (e0 + W <= n) {
+          const typename Tr::svec x =
+              __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(S)));
+#pragma unroll
+          for (int e = 0; e < W; ++e) buf[k * W + e] = (V)x[e];
+          continue;
+        }
+      }
+      const int as = mc_itemsize(a);
+#pragma unroll
+      for (int e = 0; e < W; ++e)
+        buf[k * W + e] = e0 + e < n ? Tr::from_bits(mc_load_elem_u(src, e0 + e, as), a) : (V)0;
+    }
+  };
+  auto io_store = [&](size_t t, const V *buf, int from, int step) {
+    const size_t t0 = t * (size_t)TE;
+    for (int k = from; k < NV; k += step) {
+      const size_t e0 = t0 + (size_t)k * W;
+      if (e0 >= n) break;
+      if (e0 + W <= n) {
+        typename Tr::svec x;
+#pragma unroll
+        for (int e = 0; e < W; ++e) x[e] = Tr::store(buf[k * W + e]);
+        __builtin_nontemporal_store(x, reinterpret_cast<typename Tr::svec *>(dst + e0 * sizeof(S)));
+      } else {
+        for (int e = 0; e < W && e0 + e < n; ++e) reinterpret_cast<S *>(dst)[e0 + e] = Tr::store(buf[k * W + e]);
+      }
+    }
+  };
+  io_load(tb, xs[tb & 1], threadIdx.x, MC_BLOCK);
+  __syncthreads();
+  V acc = Tr::val(yin);
+  for (size_t t = tb; t < te; ++t) {
+    if (wave == 0) {
+      if (threadIdx.x == 0) {
+        const size_t t0 = t * (size_t)TE;
+        const int cnt = (int)(n - t0 < (size_t)TE ? n - t0 : (size_t)TE);
+        V *p = xs[t & 1];
+        int j = 0;
+        if (t0 == 0 && !has_in) {  // the chunk's first element: out[0] = enc[0]
+          acc = p[0];
+          j = 1;
+        }
+        acc = fsw_chain<D>(p, j, cnt, acc);
+        if (t + 1 == te) *ldsy = Tr::store(acc);
+      }
+    } else {
+      const int io = threadIdx.x - 64;
+      if (t > tb) io_store(t - 1, xs[(t - 1) & 1], io, MC_BLOCK - 64);
+      if (t + 1 < te) io_load(t + 1, xs[(t + 1) & 1], io, MC_BLOCK - 64);
+    }
+    __syncthreads();
+  }
+  io_store(te - 1, xs[(te - 1) & 1], threadIdx.x, MC_BLOCK);
+  const S y = *ldsy;
+  __syncthreads();  // the buffers and ldsy are free again
+  return y;
+}
+
 template <int A_, int D>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restrict__ src, size_t src_stride,
                                                         uint8_t *__restrict__ dst, size_t dst_stride, size_t n,
@@ -1332,14 +1635,19 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
   using V = typename Tr::V;
   constexpr int W = Tr::W;
   constexpr int TE = (int)fs_tile<D>();
-  __shared__ double lds[FS_Q][FSW_NW];
-  __shared__ S ldsc[FS_Q][FSW_NW];
-  __shared__ uint64_t ldsf[FSW_NW];
-  __shared__ S ldsv[FSW_NW];
-  __shared__ double ldsp[FSW_NW];
+  constexpr int QE = fsw_qe<D>();
+  constexpr int NOFAIL = 0x7fffffff;
+  // per pass, each wave publishes its last candidate, its first element
+  // (value, candidate, prefix) and its first failure inside the quarter
+  __shared__ double ldsq[FSW_NW];
+  __shared__ S lds_last[2][FSW_NW], lds_bc[2][FSW_NW], lds_fv[2][FSW_NW];
+  __shared__ V lds_bv[2][FSW_NW];
+  __shared__ double lds_bp[2][FSW_NW], lds_fp[2][FSW_NW];
+  __shared__ int lds_fi[2][FSW_NW];
   __shared__ uint64_t ldsx[FSW_NW];
   __shared__ S ldsy;
-  __shared__ __attribute__((aligned(16))) V xs[TE + 2 * FSW_G];
+  __shared__ __attribute__((aligned(16))) V xs2[2][TE + 2 * FSW_G];
+  V *xs = xs2[0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool single = sums != nullptr;
   src += (size_t)blockIdx.x * src_stride;
@@ -1354,95 +1662,183 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     t = (size_t)(f / TE);
     has_in = t > 0;
     if (has_in) yin = Tr::round(pre[t - 1] + sums[t - 1]);  // tile t-1 verified: its last candidate
+  } else {
+    // a row that k_fspec_rows left at its first failing tile (rowfail = its
+    // start; n when the row verified): resume there from the last stored value
+    const uint64_t f = rowfail[blockIdx.x];
+    if (f >= n) return;
+    t = (size_t)(f / TE);
+    has_in = t > 0;
+    if (has_in) yin = reinterpret_cast<const S *>(dst)[t * (size_t)TE - 1];
   }
-  uint64_t first_rebase = n;
-  int serial_run = 0;
+  int serial_run = 0, par = 0;
   V nv[FS_Q][W];
-  fs_load<A_, D>(src, n, t * TE, a, nv);
+  fsw_load<A_, D>(src, n, t * TE, a, nv);
   while (t < ntiles) {
+    if (serial_run > 0 && (t % FSW_PROBE) != 0) {
+      // noise-like stretch: serial streaming up to the next probe tile
+      const size_t te = (t / FSW_PROBE + 1) * FSW_PROBE < ntiles ? (t / FSW_PROBE + 1) * FSW_PROBE : ntiles;
+      yin = fsw_stream<A_, D>(src, dst, n, a, t, te, yin, has_in, xs2, &ldsy);
+      has_in = true;
+      serial_run += (int)(te - t);
+      t = te;
+      if (t >= ntiles) break;
+      fsw_load<A_, D>(src, n, t * (size_t)TE, a, nv);
+      if (single && Tr::bits(yin) == Tr::bits(Tr::round(pre[t - 1] + sums[t - 1]))) {
+        const size_t nt = fsw_next_failed(tfail, t, ntiles, ldsx);
+        if (nt >= ntiles) break;
+        if (nt != t) {
+          t = nt;
+          yin = Tr::round(pre[nt - 1] + sums[nt - 1]);
+          fsw_load<A_, D>(src, n, nt * (size_t)TE, a, nv);
+        }
+        serial_run = 0;
+      }
+      continue;
+    }
     const size_t t0 = t * (size_t)TE;
     V v[FS_Q][W];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
       for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
-    if (t + 1 < ntiles) fs_load<A_, D>(src, n, t0 + TE, a, nv);  // the usual successor, in flight
-    double p[FS_Q][W];
-    fs_tile_scan<V, W>(v, p, lds);
+    if (t + 1 < ntiles) fsw_load<A_, D>(src, n, t0 + TE, a, nv);  // the usual successor, in flight
     const int cnt = (int)(n - t0 < (size_t)TE ? n - t0 : (size_t)TE);
+    const bool first_tile = t0 == 0;
     S c[FS_Q][W];
-    int fpos = -1;     // elements at local index <= fpos are final
-    S fixed = yin;     // the true value at fpos (the tile input while fpos < 0)
-    double bval = has_in ? (double)Tr::val(yin) : 0.0, bpre = 0.0;
-    bool go_serial = serial_run > 0 && (t % FSW_PROBE) != 0;
-    int steps = 0;
-    while (!go_serial) {
-      S up[FS_Q];
+    int fpos = -1;  // elements at local index <= fpos are final
+    S fixed = yin;  // the true value at fpos
+    bool go_serial = false;
+    const int cap = serial_run > 0 ? FSW_PROBE_CAP : FSW_CAP;
+    if (!go_serial) {
+      double p[FS_Q][W];
+      fsw_scan<V, W>(v, p, ldsq);
+      // candidates c_i = D(kb + p_i) with kb = y_base - p_base (one add per
+      // element; any association proposes, the check decides)
+      double kb = has_in ? (double)Tr::val(yin) : 0.0;
+      int steps = 0;
+      for (;; par ^= 1) {
+        // candidates (branch-free: every element computes, selects keep the
+        // final ones)
 #pragma unroll
-      for (int q = 0; q < FS_Q; ++q) {
+        for (int q = 0; q < FS_Q; ++q) {
 #pragma unroll
-        for (int e = 0; e < W; ++e) {
-          const int li = fsw_local(q, e, W);
-          if (li > fpos) c[q][e] = Tr::round(bval + (p[q][e] - bpre));
-          else if (li == fpos) c[q][e] = fixed;
-        }
-        up[q] = Tr::shfl_up1(c[q][W - 1]);
-        if (lane == 63) ldsc[q][wave] = c[q][W - 1];
-      }
-      __syncthreads();
-      uint64_t first = ~(uint64_t)0;
-      S fv = (S)0;
-      double fp = 0.0;
-#pragma unroll
-      for (int q = 0; q < FS_Q; ++q) {
-        const S p0 = lane ? up[q] : wave ? ldsc[q][wave - 1] : q ? ldsc[q - 1][FSW_NW - 1] : yin;
-#pragma unroll
-        for (int e = 0; e < W; ++e) {
-          const int li = fsw_local(q, e, W);
-          const size_t g = t0 + (size_t)li;
-          const S pv = e ? c[q][e - 1] : p0;
-          const S r = (g == 0) ? Tr::store(v[q][0]) : Tr::store(Tr::step(Tr::val(pv), v[q][e]));
-          const bool ok = Tr::bits(c[q][e]) == Tr::bits(r) && Tr::finite(c[q][e]);
-          if (li > fpos && li < cnt && !ok && first == ~(uint64_t)0) {
-            first = (uint64_t)li;
-            fv = r;
-            fp = p[q][e];
+          for (int e = 0; e < W; ++e) {
+            const int li = fsw_li(q, e, W);
+            const S cn = Tr::round(kb + p[q][e]);
+            c[q][e] = fsw_sel(li > fpos, cn, fsw_sel(li == fpos, fixed, c[q][e]));
           }
         }
-      }
-      uint64_t m = first;
+        // every predecessor inside the wave; the quarter's first element is
+        // checked after the barrier (its predecessor is the previous wave's).
+        // Descending order, so the smallest failing index is selected last.
+        uint32_t bm = 0;  // bit q*W+e: element (q, e) fails
+        S pvs[FS_Q];
+        {
+          S prevseg = (S)0;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(m, off, 64);
-        m = o < m ? o : m;
-      }
-      if (lane == 0) ldsf[wave] = m;
-      if (m != ~(uint64_t)0 && first == m) {  // the owner of the wave's smallest failure
-        ldsv[wave] = fv;
-        ldsp[wave] = fp;
-      }
-      __syncthreads();
-      int wm = 0;
+          for (int q = 0; q < FS_Q; ++q) {
+            const S up = fsw_up1(c[q][W - 1]);
+            pvs[q] = lane ? up : prevseg;
+            prevseg = fsw_readlane(c[q][W - 1], 63);
+          }
+        }
 #pragma unroll
-      for (int w = 1; w < FSW_NW; ++w) wm = ldsf[w] < ldsf[wm] ? w : wm;
-      const uint64_t f = ldsf[wm];
-      if (f == ~(uint64_t)0) break;  // the tile verified from the true values before it
-      if (first_rebase == n) first_rebase = t0 + f;
-      // re-base at f: numpy's value there (its predecessor is verified)
-      fpos = (int)f;
-      fixed = ldsv[wm];
-      bval = (double)Tr::val(fixed);
-      bpre = ldsp[wm];
-      if (++steps >= FSW_CAP) go_serial = true;
+        for (int q = 0; q < FS_Q; ++q) {
+#pragma unroll
+          for (int e = 0; e < W; ++e) {
+            const int li = fsw_li(q, e, W);
+            const S pe = e ? c[q][e - 1] : pvs[q];
+            const S r = Tr::store(Tr::step(Tr::val(pe), v[q][e]));
+            // non-short-circuit (&): no control flow per element
+            const bool ok = (Tr::bits(c[q][e]) == Tr::bits(r)) & Tr::finite(c[q][e]);
+            const bool bad = (!ok) & (li > fpos) & (li < cnt) & !(q == 0 && e == 0 && lane == 0);
+            bm |= (uint32_t)bad << (q * W + e);
+          }
+        }
+        // the wave's smallest failing index: lanes own interleaved vectors,
+        // so it is the lowest failing lane of the lowest segment q; its
+        // corrected value is recomputed once, by a switch on the (uniform)
+        // element position of that lane
+        int wf = NOFAIL;
+        S wv = (S)0;
+        double wp = 0.0;
+        if (__ballot(bm != 0)) {
+          int fl = 0, fk = 0;
+#pragma unroll
+          for (int q = FS_Q - 1; q >= 0; --q) {
+            const unsigned long long bal = __ballot((bm >> (q * W)) & ((1u << W) - 1));
+            if (bal) {
+              fl = __ffsll(bal) - 1;
+              fk = __builtin_ctz(((uint32_t)__builtin_amdgcn_readlane((int)bm, fl) >> (q * W))) + q * W;
+            }
+          }
+          S r = (S)0;
+          double pk = 0.0;
+#pragma unroll
+          for (int k = 0; k < FS_Q * W; ++k) {
+            if (k == fk) {  // uniform
+              const int q = k / W, e = k % W;
+              const S pe = e ? c[q][e - 1] : pvs[q];
+              r = Tr::store(Tr::step(Tr::val(pe), v[q][e]));
+              pk = p[q][e];
+            }
+          }
+          wf = wave * QE + (fk / W) * W * 64 + fl * W + fk % W;
+          wv = fsw_readlane(r, fl);
+          wp = fsw_readlane(pk, fl);
+        }
+        if (lane == 63) lds_last[par][wave] = c[FS_Q - 1][W - 1];
+        if (lane == 0) {
+          lds_bc[par][wave] = c[0][0];
+          lds_bv[par][wave] = v[0][0];
+          lds_bp[par][wave] = p[0][0];
+          lds_fi[par][wave] = wf;
+          lds_fv[par][wave] = wv;
+          lds_fp[par][wave] = wp;
+        }
+        __syncthreads();
+        // uniform: the quarters' first elements and the waves' first
+        // failures, from the last quarter down so the smallest index is
+        // selected last (all LDS reads independent)
+        int f = NOFAIL;
+        S fv = (S)0;
+        double fp = 0.0;
+#pragma unroll
+        for (int w = FSW_NW - 1; w >= 0; --w) {
+          const int wfi = lds_fi[par][w];
+          const S wfv = lds_fv[par][w], bc = lds_bc[par][w];
+          const double wfp = lds_fp[par][w], bp = lds_bp[par][w];
+          const V bv = lds_bv[par][w];
+          const S pe = w ? lds_last[par][w - 1] : yin;  // w = 0: only checked while fpos < 0
+          f = fsw_sel(wfi != NOFAIL, wfi, f);
+          fv = fsw_sel(wfi != NOFAIL, wfv, fv);
+          fp = fsw_sel(wfi != NOFAIL, wfp, fp);
+          const int lb = w * QE;
+          const S r = Tr::store((w == 0 && first_tile) ? bv : Tr::step(Tr::val(pe), bv));  // out[0] = enc[0]
+          const bool bad = (lb > fpos) & (lb < cnt) & !((Tr::bits(bc) == Tr::bits(r)) & Tr::finite(bc));
+          f = fsw_sel(bad, lb, f);
+          fv = fsw_sel(bad, r, fv);
+          fp = fsw_sel(bad, bp, fp);
+        }
+        if (f == NOFAIL) break;  // the tile verified from the true values before it
+        // re-base at f: numpy's value there (its predecessor is verified)
+        fpos = f;
+        fixed = fv;
+        kb = (double)Tr::val(fv) - fp;
+        if (++steps >= cap) {
+          go_serial = true;
+          break;
+        }
+      }
     }
     if (go_serial) {
       // serial fallback: the tile's values in element order in LDS, one lane
       // runs numpy's chain from the last true value, every lane reads back
-      if (first_rebase == n) first_rebase = t0 + (uint64_t)(fpos < 0 ? 0 : fpos);
 #pragma unroll
       for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
-        for (int e = 0; e < W; ++e) xs[fsw_local(q, e, W)] = v[q][e];
+        for (int e = 0; e < W; ++e) xs[fsw_li(q, e, W)] = v[q][e];
       __syncthreads();
       if (threadIdx.x == 0) {
         int j = fpos + 1;
@@ -1453,27 +1849,28 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           acc = xs[0];
           j = 1;
         }
-        fsw_chain<D>(xs, j, cnt, acc);
+        const V last = fsw_chain<D>(xs, j, cnt, acc);
+        ldsy = Tr::store(last);
       }
       __syncthreads();
 #pragma unroll
       for (int q = 0; q < FS_Q; ++q)
 #pragma unroll
         for (int e = 0; e < W; ++e) {
-          const int li = fsw_local(q, e, W);
+          const int li = fsw_li(q, e, W);
           if (li > fpos) c[q][e] = Tr::store(xs[li]);
           else if (li == fpos) c[q][e] = fixed;
         }
       ++serial_run;
+      yin = ldsy;
     } else {
       serial_run = 0;
+      yin = lds_last[par][FSW_NW - 1];  // the tile's last element (full tiles)
+      par ^= 1;
     }
-    fs_store<A_, D>(dst, n, t0, c);
-    if (t + 1 >= ntiles) break;
-    if (threadIdx.x == MC_BLOCK - 1) ldsy = c[FS_Q - 1][W - 1];  // the tile is full: its last element
-    __syncthreads();
-    yin = ldsy;
     has_in = true;
+    fsw_store<A_, D>(dst, n, t0, c);
+    if (t + 1 >= ntiles) break;
     if (single && Tr::bits(yin) == Tr::bits(Tr::round(pre[t] + sums[t]))) {
       // in sync with the apply pass: tiles that verified there are final
       const size_t nt = fsw_next_failed(tfail, t + 1, ntiles, ldsx);
@@ -1481,13 +1878,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
       if (nt != t + 1) {
         t = nt;
         yin = Tr::round(pre[nt - 1] + sums[nt - 1]);
-        fs_load<A_, D>(src, n, nt * (size_t)TE, a, nv);
+        fsw_load<A_, D>(src, n, nt * (size_t)TE, a, nv);
         continue;
       }
     }
     ++t;
   }
-  if (!single && threadIdx.x == 0) rowfail[blockIdx.x] = first_rebase;
 }
 
 // mc_sched.fspec = 0 disables the speculative float path (lab A/B: serial only)
@@ -1584,10 +1980,12 @@ static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int 
   }
 }
 
-// one walker per row (k_fspec_walk)
+// the speculative rows pass, then one walker per row that failed (rows that
+// verified return at once)
 template <int A_, int D>
 static void launch_fspec_rows(const uint8_t *sc, size_t src_stride, uint8_t *dc, size_t dst_stride, size_t n, int a,
                               uint64_t *fail, unsigned g, hipStream_t st) {
+  k_fspec_rows<A_, D><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
   k_fspec_walk<A_, D><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr, nullptr, nullptr,
                                             nullptr);
 }

@@ -175,12 +175,13 @@ def test_library_host_queries_need_no_gpu():
     # float f4/f8: tile totals + tile prefixes + the first-failure word of the
     # speculative scan (16 KiB of output per tile) for every float dtype and
     # any numeric astype but bool
-    assert lib.mc_delta_decode_workspace(100, 10, 10) == 3 * 8
-    assert lib.mc_delta_decode_workspace(1 << 20, 10, 10) == (2 * 256 + 1) * 8
-    assert lib.mc_delta_decode_workspace(1 << 20, 11, 11) == (2 * 512 + 1) * 8
-    assert lib.mc_delta_decode_workspace(1 << 20, 9, 9) == (2 * 128 + 1) * 8
-    assert lib.mc_delta_decode_workspace(1 << 20, 10, 11) == (2 * 512 + 1) * 8  # astype f4 -> dtype f8
-    assert lib.mc_delta_decode_workspace(100, 2, 10) == 3 * 8  # astype i2 -> dtype f4
+    # float: tile totals, tile prefixes, per-tile first failures (the walker), the first failure
+    assert lib.mc_delta_decode_workspace(100, 10, 10) == 4 * 8
+    assert lib.mc_delta_decode_workspace(1 << 20, 10, 10) == (3 * 256 + 1) * 8
+    assert lib.mc_delta_decode_workspace(1 << 20, 11, 11) == (3 * 512 + 1) * 8
+    assert lib.mc_delta_decode_workspace(1 << 20, 9, 9) == (3 * 128 + 1) * 8
+    assert lib.mc_delta_decode_workspace(1 << 20, 10, 11) == (3 * 512 + 1) * 8  # astype f4 -> dtype f8
+    assert lib.mc_delta_decode_workspace(100, 2, 10) == 4 * 8  # astype i2 -> dtype f4
     assert lib.mc_delta_decode_workspace(100, 0, 10) == 0  # bool astype: serial
     assert lib.mc_delta_decode_batch_workspace(7, 100, 10, 10) == 7 * 8
     assert lib.mc_delta_decode_batch_workspace(7, 100, 9, 11) == 7 * 8

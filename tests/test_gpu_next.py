@@ -265,6 +265,45 @@ def test_blosc_filters_fixture_frames(device):
     assert n == 84
 
 
+def test_blosc_filters_automatic_blocksize(device):
+    """blocksize=AUTOBLOCKS (numcodecs' Blosc default): the blocks c-blosc
+    chooses (compute_blocksize, pinned by the frame headers in
+    tests/test_oracle_next.py) -- the frames of arrays 05-12 are reproduced
+    from the config alone, and large buffers are cut as the rule says."""
+    from numcodecs_amd import blosc_shuffle as bsh
+    from oracle import blosc
+
+    n = 0
+    ncodecs = 13
+    for k, (arr, _j, config, frame) in enumerate(fixture_cases("blosc")):
+        if k // ncodecs <= 4 and config["blocksize"] == 0:
+            continue  # written by an older c-blosc (tests/test_oracle_next.py)
+        try:
+            flags, ts, bs, blocks = blosc.frame_filtered_blocks(frame)
+        except NotImplementedError:  # not an LZ4 frame
+            continue
+        if blocks is None:
+            continue
+        mode = 2 if flags & blosc.BLOSC_DOBITSHUFFLE else 1 if flags & blosc.BLOSC_DOSHUFFLE else 0
+        raw = arr.tobytes(order="A")
+        # a forced blocksize reaches the frame as c-blosc clamps it (256 -> 255 for typesize 3)
+        forced = config["blocksize"] and bsh.compute_blocksize(len(raw), ts, config["clevel"], config["cname"],
+                                                                config["blocksize"])
+        got = bsh.shuffle(np.frombuffer(raw, "u1"), ts, forced or bsh.AUTOBLOCKS, mode, config["clevel"],
+                          config["cname"])
+        assert got.tobytes() == b"".join(blocks), (k, ts, bs, mode)
+        n += 1
+    assert n > 40
+    for ts, clevel, cname in ((4, 5, "lz4"), (8, 9, "zstd"), (2, 1, "blosclz"), (4, 0, "lz4")):
+        raw = RNG.integers(0, 256, (4 << 20) + 3 * ts, dtype=np.uint8)
+        xd = torch.from_numpy(raw).to(device)
+        bs = bsh.compute_blocksize(raw.size, ts, clevel, cname)
+        for mode in (1, 2):
+            got = bsh.shuffle(xd, ts, mode=mode, clevel=clevel, cname=cname)
+            assert got.cpu().numpy().tobytes() == blosc.blosc_filter(raw, ts, bs, mode), (ts, clevel, cname, mode)
+            assert torch.equal(bsh.unshuffle(got, ts, mode=mode, clevel=clevel, cname=cname), xd)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 def test_blosc_filters_sizes(device, mode):
     from numcodecs_amd import blosc_shuffle as bsh

@@ -5,7 +5,9 @@ packbits.py/astype.py docstrings) and, where the reference is importable
 here, against the reference's compiled jenkins.pyx and Python modules.
 """
 
+import os
 import zlib
+from glob import glob
 
 import numpy as np
 import pytest
@@ -15,7 +17,7 @@ try:  # the reference loader stays in this container (.gpurunignore)
     from oracle import refload
 except ImportError:  # GPU box
     refload = None
-from tests.helpers import fixture_cases
+from tests.helpers import FIXTURE, fixture_cases
 
 RNG = np.random.default_rng(77)
 
@@ -184,3 +186,47 @@ def test_blosc_filter_roundtrip_edges():
                     enc = blosc.blosc_filter(raw, ts, bs, mode)
                     assert len(enc) == len(raw)
                     assert blosc.blosc_filter(enc, ts, bs, mode, forward=False) == raw
+
+
+def test_blosc_compute_blocksize_pinned_by_fixture_headers():
+    """numcodecs_amd.blosc_shuffle.compute_blocksize (c-blosc's
+    compute_blocksize restated; host logic, no device) against the blocksize
+    in every fixture/blosc frame header it covers: the frames the current
+    c-blosc wrote (arrays 05-12, automatic blocksize) and every frame with a
+    forced blocksize.  Arrays 00-04 with an automatic blocksize were written
+    by an older c-blosc (128/256-byte blocks for <= 8 KB buffers) and are
+    reported, not matched."""
+    from numcodecs_amd.blosc_shuffle import compute_blocksize
+    from oracle import blosc
+
+    checked = old = 0
+    ncodecs = len(glob(os.path.join(FIXTURE, "blosc", "codec.*")))
+    for k, (arr, j, config, frame) in enumerate(fixture_cases("blosc")):
+        i = k // ncodecs  # the array index (arrays outer, codecs inner)
+        flags, ts, nbytes, bs, _cb = blosc.frame_header(frame)
+        got = compute_blocksize(nbytes, ts, config["clevel"], config["cname"], config["blocksize"])
+        if config["blocksize"] == 0 and i <= 4:
+            old += 1
+            continue
+        assert got == bs, (i, j, config, ts, nbytes, bs, got)
+        checked += 1
+    assert checked == 8 * 11 + 13 * 2 and old == 5 * 11
+
+
+def test_blosc_compute_blocksize_rules():
+    """The branches the fixtures cannot reach (buffers >= 32 KiB): c-blosc's
+    published rule, parity unpinned (c-blosc is absent here)."""
+    from numcodecs_amd.blosc_shuffle import compute_blocksize
+
+    MiB = 1 << 20
+    assert compute_blocksize(256 * MiB, 4, 5, "lz4") == 524288  # L1 x 4 = 128 KiB, split: x typesize
+    assert compute_blocksize(256 * MiB, 4, 5, "zstd") == 262144  # HCR x 2, never split
+    assert compute_blocksize(256 * MiB, 4, 9, "zlib") == 1 << 20  # HCR, clevel 9, split, capped at 1 MiB
+    assert compute_blocksize(256 * MiB, 4, 0, "lz4") == 8192  # clevel 0: L1 / 4, no split at clevel 0
+    assert compute_blocksize(256 * MiB, 32, 5, "lz4") == 131072  # typesize > 16: no split
+    assert compute_blocksize(256 * MiB, 3, 1, "blosclz") == 65535  # 16 KiB x 3, raised to 64 KiB, multiple of 3
+    assert compute_blocksize(100, 300, 5, "lz4") == 100  # typesize > 255 counts as 1
+    assert compute_blocksize(3, 4, 5, "lz4") == 1  # fewer bytes than one element
+    assert compute_blocksize(10000, 4, 5, "lz4", 64) == 128  # forced sizes are at least 128
+    with pytest.raises(ValueError):
+        compute_blocksize(100, 4, 10)

@@ -19,6 +19,7 @@ from tests.test_gpu_delta_walk import family  # noqa: E402
 
 dt = sys.argv[1] if len(sys.argv) > 1 else "f4"
 mib = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+quick = len(sys.argv) > 3 and sys.argv[3] == "quick"  # single chunk only, no batches
 npdt = np.dtype("<" + dt)
 tdt = {"f4": torch.float32, "f8": torch.float64}[dt]
 dev = torch.device("cuda", 0)
@@ -59,7 +60,7 @@ for kind in ("smooth", "sin4096", "sin_noise", "randwalk", "chirp", "sparse", "s
     del encs, dst
 # batches: 2048 x 1 MiB (fewer for the random rows)
 rows_n = (1 << 20) // npdt.itemsize
-for kind, rows in (("smooth", 2048), ("sin_noise", 2048), ("randwalk", 2048), ("randn", 512)):
+for kind, rows in [] if quick else (("smooth", 2048), ("sin_noise", 2048), ("randwalk", 2048), ("randn", 512)):
     xs = np.stack([family(kind, rows_n, seed=k % 16).astype(npdt) for k in range(16)])
     enc_h = np.empty_like(xs)
     enc_h[:, 0] = xs[:, 0]
