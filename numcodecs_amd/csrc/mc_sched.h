@@ -27,6 +27,7 @@ struct mc_sched_t {
   int dscan_nt;        // k_dscan two-launch decode: bit 0 nt reduce loads, bit 1 nt apply loads
   int fspec;           // speculative float Delta decode (0 = serial chain only)
   int fastdiv;         // FSO decode divides by the constant scale with the Markstein rcp (0/1)
+  int crc_lds;         // CRC32/CRC32C tiles of >= 4 vectors per lane fold with the LDS slicing-by-16 tables (1) or bit-sliced XORs (0)
 };
 
 extern mc_sched_t mc_sched __attribute__((visibility("hidden")));

@@ -26,6 +26,7 @@ import torch  # noqa: E402
 import oracle  # noqa: E402
 from numcodecs_amd import (  # noqa: E402
     CRC32,
+    CRC32C,
     Adler32,
     Delta,
     FixedScaleOffset,
@@ -59,12 +60,12 @@ def check_checksums():
     for n in ((1 << 22) + 7, 3 << 20, 1000):
         x = rng.integers(0, 256, n, dtype=np.uint8)
         xd = torch.from_numpy(x).to(dev)
-        for codec, cid in ((CRC32(), "crc32"), (Adler32(), "adler32")):
+        for codec, cid in ((CRC32(), "crc32"), (CRC32C(), "crc32c"), (Adler32(), "adler32")):
             enc = codec.encode(xd)
             ok &= _h(enc) == oracle.checksum32_encode(cid, x).tobytes()
             ok &= _h(codec.decode(enc)) == x.tobytes()
     rows = torch.from_numpy(rng.integers(0, 256, (6, 1 << 20), dtype=np.uint8)).to(dev)
-    for cid in ("crc32", "adler32"):
+    for cid in ("crc32", "crc32c", "adler32"):
         enc = batch.checksum32_encode_chunks(rows, cid)
         eh = enc.cpu().numpy()
         for i in range(6):
@@ -157,6 +158,7 @@ PLAN = {
     "dscan_nt": ([0, 1, 3], check_delta_int),
     "fspec": ([0], check_delta_float),
     "fastdiv": ([0], check_fso),
+    "crc_lds": ([1], check_checksums),
 }
 
 

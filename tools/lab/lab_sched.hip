@@ -37,6 +37,7 @@ const field kFields[] = {
     {"dscan_nt", "MCODEC_DSCAN_NT", &mc_sched.dscan_nt},
     {"fspec", "MCODEC_FSPEC", &mc_sched.fspec},
     {"fastdiv", "MCODEC_FASTDIV", &mc_sched.fastdiv},
+    {"crc_lds", "MCODEC_CRC_LDS", &mc_sched.crc_lds},
 };
 
 __attribute__((constructor)) void lab_sched_from_env() {
