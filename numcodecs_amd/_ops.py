@@ -376,6 +376,30 @@ def fletcher32_decode_device(buf: torch.Tensor):
     return payload, val, found
 
 
+def checksum32_decode_device(kind, buf: torch.Tensor, init, location):
+    """Checksum32.decode (CRC32 / CRC32C / Adler32) of a flat contiguous
+    uint8 device tensor on the current device, launch first as
+    fletcher32_decode_device: (payload, computed, stored), or None for the
+    general path (other device, HIP-graph capture, too short)."""
+    n = buf.numel()
+    idx = buf.get_device()
+    if n <= 4 or _raw_stream is None or _cur_device is None or idx != _cur_device():
+        return None
+    st = _raw_stream(idx)
+    sl = _verify_slot(buf, st)
+    if sl is None:
+        return None
+    ws = sl.workspace_for((kind, n), lambda: lib.mc_checksum32_workspace(kind, 1, n - 4))
+    seq = sl.next_seq()
+    rc = lib.mc_checksum32_verify_fused(kind, buf.data_ptr(), n, init, None, 0, location, sl.out_ptr, seq,
+                                        ws.data_ptr(), ws.numel(), sl.ticket_ptr, st)
+    if rc:
+        check(rc, "mc_checksum32_verify_fused")
+    payload = buf[4:] if location == _native.MC_CK_START else buf[: n - 4]  # while the kernel runs
+    val, found = sl.read(st, seq)
+    return payload, val, found
+
+
 def fletcher32(src, nbytes) -> int:
     """Checksum of the first `nbytes` of a device tensor (syncs)."""
     _native.require_device()

@@ -181,12 +181,19 @@ MC_DEV void adler_arrive_finish(uint32_t a1, uint32_t a2, size_t n, const uint8_
       atomicAdd(t, ((unsigned long long)s2 << 32) | ((unsigned long long)s1 << 8) | 1ull);
   if ((top & 0xffu) + 1u != mc_arrival_nshards(gridDim.x)) return;
   *t = 0;
-  const uint64_t x = (((top >> 8) & 0xffffffu) + s1) % ADLER_P;
-  const uint64_t y = (((top >> 32) & 0xffffffu) + s2) % ADLER_P;
+  uint64_t x = (((top >> 8) & 0xffffffu) + s1) % ADLER_P;
+  uint64_t y = (((top >> 32) & 0xffffffu) + s2) % ADLER_P;
+  // head: the tiles started at the 4 stored bytes (byte j weighted n - j); take them out
+  for (uint32_t j = 0; j < fx.head; ++j) {
+    const uint64_t dj = fx.stored[j];
+    x = (x + ADLER_P - dj) % ADLER_P;
+    y = (y + ADLER_P - (uint64_t)((n - j) % ADLER_P) * dj % ADLER_P) % ADLER_P;
+  }
+  const size_t np = n - fx.head;  // payload bytes
   // zlib.adler32(data, value): a0 = value & 0xffff, b0 = value >> 16
   const uint64_t a0 = fx.init & 0xffffu, b0 = fx.init >> 16;
   const uint64_t a = (a0 + x) % ADLER_P;
-  const uint64_t b = (b0 + (n % ADLER_P) * a0 + y) % ADLER_P;
+  const uint64_t b = (b0 + (np % ADLER_P) * a0 + y) % ADLER_P;
   const uint32_t result = (uint32_t)((b << 16) | a);
   if (fx.stored_out) fx.stored_out[0] = load_le32(fx.stored);
   if (fx.out) fx.out[0] = result;
@@ -428,9 +435,11 @@ struct HostPow {
   }
 };
 
+// n: bytes the tiles cover; np: payload bytes (n - 4 with a head, else n)
 template <int KIND>
-CrcFin crc_fin_build(int K, size_t tpc, size_t n) {
+CrcFin crc_fin_build(int K, size_t tpc, size_t n, size_t np) {
   CrcFin f{};
+  f.head = n != np;
   if constexpr (KIND != K_ADLER) {
     constexpr uint32_t poly = crc_poly<KIND>();
     static const HostPow hp(poly);
@@ -455,7 +464,7 @@ CrcFin crc_fin_build(int K, size_t tpc, size_t n) {
       f.tail[t] = step == 0 ? f.tail[t + 1] : gf_mul(f.tail[t + 1], step == d0 ? m0 : m1, poly);
     }
     f.pad = HostPow::pw(hp.x2n_inv, 8 * (tb * tpc - n), poly);
-    f.xn = HostPow::pw(hp.x2n, 8 * (uint64_t)n, poly);
+    f.xn = HostPow::pw(hp.x2n, 8 * (uint64_t)np, poly);
   }
   return f;
 }
@@ -463,17 +472,18 @@ CrcFin crc_fin_build(int K, size_t tpc, size_t n) {
 // the constants of the last call on this thread (a stream of equal-size
 // chunks asks for the same ones every time)
 template <int KIND>
-const CrcFin &crc_fin(int K, size_t tpc, size_t n) {
+const CrcFin &crc_fin(int K, size_t tpc, size_t n, size_t np) {
   thread_local struct {
     int K = -1;
-    size_t tpc = 0, n = 0;
+    size_t tpc = 0, n = 0, np = 0;
     CrcFin f;
   } last;
-  if (KIND != K_ADLER && (last.K != K || last.tpc != tpc || last.n != n)) {
-    last.f = crc_fin_build<KIND>(K, tpc, n);
+  if (KIND != K_ADLER && (last.K != K || last.tpc != tpc || last.n != n || last.np != np)) {
+    last.f = crc_fin_build<KIND>(K, tpc, n, np);
     last.K = K;
     last.tpc = tpc;
     last.n = n;
+    last.np = np;
   }
   return last.f;
 }
@@ -482,7 +492,11 @@ template <int KIND>
 int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks, size_t n,
                   uint32_t init, uint32_t *out, uint8_t *footer, size_t fs, const uint8_t *stored,
                   uint32_t *stored_out, void *ws, size_t ws_bytes, hipStream_t st, uint32_t *ticket,
-                  uint32_t seq) {
+                  uint32_t seq, uint32_t head) {
+  // head = 4: s is the 16-B aligned buffer start, 4 stored bytes before the
+  // n payload bytes; the tiles cover all n + 4 (one-launch verify only)
+  const size_t np = n;
+  n += head;
   const int K = ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
@@ -490,11 +504,11 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   uint32_t *parts = static_cast<uint32_t *>(ws);
   // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
   const bool fused = ticket && nchunks == 1;
-  const CkFinish fx{init, seq, ticket, out, stored_out, footer, fs, stored};
+  const CkFinish fx{init, seq, head, ticket, out, stored_out, footer, fs, stored};
   switch (K) {
 #define MC_CK_CASE(KK)                                                                         \
   case KK: {                                                                                   \
-    const CrcFin &fin = crc_fin<KIND>(KK, tpc, n);                                             \
+    const CrcFin &fin = crc_fin<KIND>(KK, tpc, n, np);                                         \
     dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, fin, fused ? &fx : nullptr, st); \
     if (!fused)                                                                                \
       k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                         \
@@ -515,17 +529,18 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
 int ck_dispatch(int kind, const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nchunks,
                 size_t n, uint32_t init, const uint8_t *prefix, size_t plen, uint32_t *out,
                 uint8_t *footer, size_t fs, const uint8_t *stored, uint32_t *stored_out, void *ws,
-                size_t ws_bytes, hipStream_t st, uint32_t *ticket = nullptr, uint32_t seq = 0) {
+                size_t ws_bytes, hipStream_t st, uint32_t *ticket = nullptr, uint32_t seq = 0,
+                uint32_t head = 0) {
   switch (kind) {
     case MC_CK_CRC32:
       return run_reduction<K_CRC32>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st, ticket, seq);
+                                    ws, ws_bytes, st, ticket, seq, head);
     case MC_CK_CRC32C:
       return run_reduction<K_CRC32C>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                     ws, ws_bytes, st, ticket, seq);
+                                     ws, ws_bytes, st, ticket, seq, head);
     case MC_CK_ADLER32:
       return run_reduction<K_ADLER>(s, ss, d, ds, nchunks, n, init, out, footer, fs, stored, stored_out,
-                                    ws, ws_bytes, st, ticket, seq);
+                                    ws, ws_bytes, st, ticket, seq, head);
     case MC_CK_JENKINS: {
       if (d && n) {
         const int rc = mc_copy_rows_impl(s, ss, d, ds, n, nchunks, st);
@@ -549,7 +564,10 @@ extern "C" {
 
 size_t mc_checksum32_workspace(int kind, size_t nchunks, size_t chunk_bytes) {
   if (!valid_kind(kind) || kind == MC_CK_JENKINS) return 0;
-  const size_t tpc = ck_tiles(chunk_bytes, ck_k_ws(chunk_bytes));
+  // a one-launch verify may tile the stored word with the payload (+ 4)
+  const size_t t0 = ck_tiles(chunk_bytes, ck_k_ws(chunk_bytes));
+  const size_t t4 = ck_tiles(chunk_bytes + 4, ck_k_ws(chunk_bytes + 4));
+  const size_t tpc = t0 > t4 ? t0 : t4;
   return tpc * nchunks * (kind == MC_CK_ADLER32 ? 8 : 4);
 }
 
@@ -644,6 +662,13 @@ int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes, 
   const uint8_t *s = static_cast<const uint8_t *>(src);
   const uint8_t *payload = location == MC_CK_START ? s + 4 : s;
   const uint8_t *stored = location == MC_CK_START ? s : s + n;
+  // location "start" on a 16-B aligned buffer: the payload at +4 would be read
+  // with dword-aligned vectors; the one-launch CRC / Adler32 verify instead
+  // tiles the whole aligned buffer and removes the stored word's share at its
+  // finish (CrcFin::head, adler_arrive_finish)
+  if (ticket && location == MC_CK_START && kind != MC_CK_JENKINS && ((uintptr_t)s & 15) == 0 && n >= 16)
+    return ck_dispatch(kind, s, encoded_bytes, nullptr, 0, 1, n, init, nullptr, 0, out_pair, nullptr, 0, stored,
+                       out_pair + 1, workspace, workspace_bytes, (hipStream_t)stream, ticket, seq, 4);
   return ck_dispatch(kind, payload, encoded_bytes, nullptr, 0, 1, n, init, static_cast<const uint8_t *>(prefix),
                      prefix_bytes, out_pair, nullptr, 0, stored, out_pair + 1, workspace, workspace_bytes,
                      (hipStream_t)stream, ticket, seq);

@@ -1336,8 +1336,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
 // value; rowfail[row] = the first index that needed a re-basing (n if none).
 // ---------------------------------------------------------------------------
 constexpr int FSW_CAP = 16;        // re-basings per tile before the serial fallback
-constexpr int FSW_PROBE = 8;       // after a serial tile, every FSW_PROBE-th tile speculates again ...
-constexpr int FSW_PROBE_CAP = 2;   // ... with at most this many re-basings
+constexpr int FSW_PROBE = 8;       // after a serial tile, the FSW_PROBE-th tile on speculates again ...
+constexpr int FSW_PROBE_CAP = 2;   // ... with at most this many re-basings; each failed probe doubles
+constexpr int FSW_PROBE_MAX = 64;  // the gap up to this (noise costs ~0.5 % over the plain chain)
 constexpr int FSW_G = 32;          // serial chain: values per LDS read group (8 x 16 B in flight)
 constexpr int FSW_NW = MC_BLOCK / 64;
 
@@ -1672,12 +1673,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     if (has_in) yin = reinterpret_cast<const S *>(dst)[t * (size_t)TE - 1];
   }
   int serial_run = 0, par = 0;
+  size_t next_probe = 0, gap = FSW_PROBE;  // serial tiles stream until next_probe
   V nv[FS_Q][W];
   fsw_load<A_, D>(src, n, t * TE, a, nv);
   while (t < ntiles) {
-    if (serial_run > 0 && (t % FSW_PROBE) != 0) {
+    if (serial_run > 0 && t < next_probe) {
       // noise-like stretch: serial streaming up to the next probe tile
-      const size_t te = (t / FSW_PROBE + 1) * FSW_PROBE < ntiles ? (t / FSW_PROBE + 1) * FSW_PROBE : ntiles;
+      const size_t te = next_probe < ntiles ? next_probe : ntiles;
       yin = fsw_stream<A_, D>(src, dst, n, a, t, te, yin, has_in, xs2, &ldsy);
       has_in = true;
       serial_run += (int)(te - t);
@@ -1693,6 +1695,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           fsw_load<A_, D>(src, n, nt * (size_t)TE, a, nv);
         }
         serial_run = 0;
+        gap = FSW_PROBE;
       }
       continue;
     }
@@ -1861,10 +1864,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           if (li > fpos) c[q][e] = Tr::store(xs[li]);
           else if (li == fpos) c[q][e] = fixed;
         }
+      if (serial_run > 0) gap = gap * 2 < (size_t)FSW_PROBE_MAX ? gap * 2 : (size_t)FSW_PROBE_MAX;  // probe failed
       ++serial_run;
+      next_probe = t + gap;
       yin = ldsy;
     } else {
       serial_run = 0;
+      gap = FSW_PROBE;
       yin = lds_last[par][FSW_NW - 1];  // the tile's last element (full tiles)
       par ^= 1;
     }
