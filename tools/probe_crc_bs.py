@@ -60,6 +60,13 @@ SETTINGS = {
     "bs_grid1024": {"MCODEC_CK_GRID": "1024", "MCODEC_CK_GRID_COPY": "1024"},
     "bs_grid2048": {"MCODEC_CK_GRID": "2048", "MCODEC_CK_GRID_COPY": "2048"},
     "bs_k8": {"MCODEC_CK_K": "8"},
+    "bs_k8_grid768": {"MCODEC_CK_K": "8", "MCODEC_CK_GRID": "768"},
+    "bs_k8_grid1024": {"MCODEC_CK_K": "8", "MCODEC_CK_GRID": "1024"},
+    "bs_k8_grid2048": {"MCODEC_CK_K": "8", "MCODEC_CK_GRID": "2048"},
+    "bs_grid4096": {"MCODEC_CK_GRID": "4096", "MCODEC_CK_GRID_COPY": "4096"},
+    "bs_kcopy16_grid512": {"MCODEC_CK_KCOPY": "16", "MCODEC_CK_GRID_COPY": "512"},
+    "bs_gridcopy512": {"MCODEC_CK_GRID_COPY": "512"},
+    "bs_gridcopy768": {"MCODEC_CK_GRID_COPY": "768"},
     "bs_kcopy16": {"MCODEC_CK_KCOPY": "16"},
 }
 
