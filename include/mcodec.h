@@ -386,7 +386,10 @@ int mc_checksum32_encode_fused(int kind, const void *src, void *dst,
  * out_pair[1] = the stored LE32 value (the caller compares and raises).
  * `ticket`, out_pair and seq as for mc_fletcher32_verify_fused (seq != 0
  * needs a ticket and is refused for Jenkins, which has no one-launch fold);
- * workspace: mc_checksum32_workspace(kind, 1, encoded_bytes - 4). */
+ * workspace: mc_checksum32_workspace(kind, 1, encoded_bytes - 4), which also
+ * covers the aligned path: with location MC_CK_START, a ticket and a 16-B
+ * aligned src, CRC32 / CRC32C / Adler32 read the whole buffer with aligned
+ * vectors and remove the stored word's share at the finish (same result). */
 int mc_checksum32_verify_fused(int kind, const void *src, size_t encoded_bytes,
                                uint32_t init, const void *prefix,
                                size_t prefix_bytes, int location,
