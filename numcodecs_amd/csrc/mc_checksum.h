@@ -89,24 +89,6 @@ MC_DEV const CrcConsts &crc_consts() {
 template <int KIND>
 constexpr uint32_t crc_poly() { return KIND == K_CRC32C ? POLY_CRC32C : POLY_CRC32; }
 
-// The lane's fold of K >= 4 vectors without table lookups (mc_crc_bs.h,
-// generated by gen_crc_bs.py): the 32 bit positions of the loaded dwords are
-// 32 independent streams, so the fold is a fixed XOR network over the dwords
-// (4K inputs -> 32 words, four Russians + v_bitop3 XOR3) and a 31-step
-// Horner -- about 2.5 VALU ops per byte for K = 16 where the table fold
-// spends 16 LDS lookups per 16 B at ~4-way bank conflicts.
-template <int KIND, int K>
-MC_DEV uint32_t crc_fold_bs(const mc_u32x4 *v) {
-  if constexpr (KIND == K_CRC32C) {
-    if constexpr (K == 4) return crc_bs_crc32c_k4(v);
-    else if constexpr (K == 8) return crc_bs_crc32c_k8(v);
-    else return crc_bs_crc32c_k16(v);
-  } else {
-    if constexpr (K == 4) return crc_bs_crc32_k4(v);
-    else if constexpr (K == 8) return crc_bs_crc32_k8(v);
-    else return crc_bs_crc32_k16(v);
-  }
-}
 
 // acc = raw(acc, v ++ zeros(SHIFT)) with the 16 LDS tables
 MC_DEV uint32_t slice16(const uint32_t *__restrict__ V, uint32_t acc, mc_u32x4 v) {
@@ -386,19 +368,6 @@ MC_DEV uint32_t mulx_r(uint32_t a) {  // a * x mod P (reflected)
   return (a >> 1) ^ ((uint32_t)__builtin_amdgcn_sbfe((int)a, 0, 1) & crc_poly<KIND>());
 }
 
-template <int K, int ALS>
-MC_DEV void ck_load_tile(mc_u32x4 (&v)[K], const uint8_t *s, size_t base, size_t n, bool full) {
-  if (full) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = ld_vec<ALS>(s + base + (size_t)k * STEP);
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const size_t pos = base + (size_t)k * STEP;
-      v[k] = pos < n ? ld_masked<ALS>(s, pos, n) : mc_u32x4{0, 0, 0, 0};
-    }
-  }
-}
 
 // bit-sliced CRC tiles (mc_crc_bs.hip): the kernel for tiles of K >= 4
 // vectors per lane; kind MC_CK_CRC32 / MC_CK_CRC32C, als / ald = align class
