@@ -106,13 +106,11 @@ def reference(dwords, K, poly):
     return raw(0, msg, poly)
 
 
-def network(K, poly, g_lo, g_hi, init):
-    """XOR-network lines for vector groups [g_lo, g_hi) of a K-vector lane:
-    w[i] ^= (or, with init, =) the XOR of the dwords whose column has
-    coefficient i.  Four Russians per group, two groups per XOR3."""
+def emit(name, K, poly):
     z = columns(K, poly)
-    lines = []
-    for k in range(g_lo, g_hi):
+    J = 4 * K
+    lines = [f"MC_DEV uint32_t {name}(const mc_u32x4 *__restrict__ v) {{"]
+    for k in range(K):
         lines.append(f"  const uint32_t d{4*k} = v[{k}].x, d{4*k+1} = v[{k}].y, "
                      f"d{4*k+2} = v[{k}].z, d{4*k+3} = v[{k}].w;")
     # pattern of output i in group g: bit b set when dword 4g+b feeds W_i
@@ -147,9 +145,9 @@ def network(K, poly, g_lo, g_hi, init):
             get(m)
         return names, out
 
-    started = [not init] * 32
-    for g0 in range(g_lo, g_hi, 2):
-        gs = [g for g in (g0, g0 + 1) if g < g_hi]
+    started = [False] * 32
+    for g0 in range(0, K, 2):
+        gs = [g for g in (g0, g0 + 1) if g < K]
         tables = []
         for g in gs:
             names, out = combos(g)
@@ -163,47 +161,22 @@ def network(K, poly, g_lo, g_hi, init):
                 started[i] = True
                 expr = terms[0] if len(terms) == 1 else f"{terms[0]} ^ {terms[1]}"
                 nops += len(terms) - 1
-                lines.append(f"  w[{i}] = {expr};")
+                lines.append(f"  uint32_t w{i} = {expr};")
             elif len(terms) == 2:
-                lines.append(f"  w[{i}] = X3(w[{i}], {terms[0]}, {terms[1]});")
+                lines.append(f"  w{i} = X3(w{i}, {terms[0]}, {terms[1]});")
                 nops += 1
             elif len(terms) == 1:
-                lines.append(f"  w[{i}] ^= {terms[0]};")
+                lines.append(f"  w{i} ^= {terms[0]};")
                 nops += 1
     for i in range(32):
         if not started[i]:
-            lines.append(f"  w[{i}] = 0;")
-    return lines, nops
-
-
-def emit(name, K, poly):
-    """name_part0 / name_part1: the network over the first / second half of
-    the lane's vectors (part0 initialises w); name: both halves + Horner."""
-    out, nops = [], 0
-    for part, (lo, hi) in enumerate(((0, K // 2), (K // 2, K))):
-        lines, n = network(K, poly, lo, hi, init=part == 0)
-        nops += n
-        out += [f"MC_DEV void {name}_part{part}(uint32_t (&w)[32], const mc_u32x4 *__restrict__ v) {{"] + lines
-        out += ["}", ""]
-    out += [f"MC_DEV uint32_t {name}(const mc_u32x4 *__restrict__ v) {{",
-            "  uint32_t w[32];",
-            f"  {name}_part0(w, v);",
-            f"  {name}_part1(w, v);",
-            f"  return {horner_name(poly)}(w);",
-            "}"]
-    return out, nops
-
-
-def horner_name(poly):
-    return "crc_bs_horner_" + [k for k, v in POLYS.items() if v == poly][0]
-
-
-def emit_horner(poly):
-    lines = [f"// acc = XOR_i x^i * w[i] (w[i] read as a polynomial): 31 steps of a*x ^ w",
-             f"MC_DEV uint32_t {horner_name(poly)}(const uint32_t (&w)[32]) {{", "  uint32_t acc = w[31];"]
+            lines.append(f"  const uint32_t w{i} = 0;")
+    lines.append(f"  uint32_t acc = w31;")
     for i in range(30, -1, -1):
-        lines.append(f"  acc = MULX_XOR(acc, w[{i}], 0x{poly:08X}u);")
-    return lines + ["  return acc;", "}", ""]
+        lines.append(f"  acc = MULX_XOR(acc, w{i}, 0x{poly:08X}u);")
+    lines.append("  return acc;")
+    lines.append("}")
+    return lines, nops
 
 
 def main():
@@ -220,8 +193,6 @@ def main():
                     d[rng.randrange(4 * K)] = 1 << rng.randrange(32)
                 assert model(d, K, poly) == reference(d, K, poly), (pname, K, trial)
             name = f"crc_bs_{pname}_k{K}"
-            if K == KS[0]:
-                body += emit_horner(poly)
             lines, nops = emit(name, K, poly)
             stats.append(f"//   {name}: {nops} XOR-network ops + 31 Horner steps for {16 * K} bytes per lane")
             body += lines + [""]
