@@ -172,12 +172,18 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec(
 // ---------------------------------------------------------------------------
 // es = 8 with lane pairs: every lane moves 16 B per access on the element side
 // (2 elements, lane-contiguous: 1 KiB per wave instruction).  Lanes 2m and
-// 2m+1 hold elements 4m..4m+1 and 4m+2..4m+3; one __shfl_xor(., 1) exchange
+// 2m+1 hold elements 4m..4m+1 and 4m+2..4m+3; one pair-swap exchange
 // gives the even lane the low dwords and the odd lane the high dwords of the
 // 4 elements, and a 4x4 byte transpose turns them into plane dwords 0-3 (even)
 // and 4-7 (odd).  A plane store instruction therefore writes two 128-B runs.
 // Tile = 256 lanes x NV 16-B units.
 // ---------------------------------------------------------------------------
+// value of the partner lane (lane ^ 1): one DPP quad_perm [1,0,3,2] move
+// (__shfl_xor(v, 1) compiles to an LDS ds_bpermute round trip)
+MC_DEV uint32_t mc_pair_swap(uint32_t v) {  // value of the partner lane (lane ^ 1)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
 template <bool BITROUND, bool NT, int NV>
 __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair(
     const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
@@ -201,8 +207,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair(
         uint64_t e1 = mc_bitround64(((uint64_t)x.w << 32) | x.z, br);
         x = mc_u32x4{(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32)};
       }
-      const uint32_t a = __shfl_xor(odd ? x.x : x.y, 1, 64);
-      const uint32_t b = __shfl_xor(odd ? x.z : x.w, 1, 64);
+      const uint32_t a = mc_pair_swap(odd ? x.x : x.y);
+      const uint32_t b = mc_pair_swap(odd ? x.z : x.w);
       uint32_t p0, p1, p2, p3;
       if (odd) mc_tr4(a, b, x.y, x.w, p0, p1, p2, p3);   // high dwords of e0..e3
       else mc_tr4(x.x, x.z, a, b, p0, p1, p2, p3);       // low dwords of e0..e3
@@ -239,8 +245,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
     for (int r = 0; r < NV; ++r) {
       uint32_t w0, w1, w2, w3;  // even: low dwords of e0..e3; odd: high dwords
       mc_tr4(pl[r][0], pl[r][1], pl[r][2], pl[r][3], w0, w1, w2, w3);
-      const uint32_t a = __shfl_xor(odd ? w0 : w2, 1, 64);
-      const uint32_t b = __shfl_xor(odd ? w1 : w3, 1, 64);
+      const uint32_t a = mc_pair_swap(odd ? w0 : w2);
+      const uint32_t b = mc_pair_swap(odd ? w1 : w3);
       const mc_u32x4 o = odd ? mc_u32x4{a, w2, b, w3} : mc_u32x4{w0, a, w1, b};
       mc_st16<NT>(d + ((size_t)r * MC_BLOCK + tid) * 16, o);
     }
@@ -256,9 +262,6 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
 // plane instructions instead of 4.  Element side unchanged (16 B per lane,
 // lane-contiguous).
 // ---------------------------------------------------------------------------
-MC_DEV uint32_t mc_pair_swap(uint32_t v) {  // value of the partner lane (lane ^ 1)
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-}
 
 template <bool BITROUND, bool NT, int QMUL>
 __global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_enc_pair(
