@@ -54,7 +54,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
     for (int k = 0; k < 4; ++k) a[k] = fso_enc<D, A>(x[q][k], p);
     // the element before the quad is the last one of lane - 1's quad; lane 0
     // reads it (A is at most 32 bits wide, so differences mod 2^32 suffice)
-    int64_t prev = (int64_t)(int32_t)__shfl_up((uint32_t)a[3], 1, 64);
+    int64_t prev = (int64_t)(int32_t)mc_wave_shr1((uint32_t)a[3], 0u);
     if (lane == 0 && e > 0 && e < p.n) prev = fso_enc<D, A>(mc_load_elem(src, e - 1, DS), p);
     if (e >= p.n) continue;
     d[0] = e > 0 ? mc_wrap(a[0] - prev, A) : a[0];

@@ -34,6 +34,12 @@ typedef uint32_t mc_u32x2 __attribute__((ext_vector_type(2)));
 // Global streaming accesses.  NT = nontemporal (`nt` bit): measured on MI355X
 // (tools/bwtest.hip, profiles/) a 16-B/lane copy streams at 6.4-6.5 TB/s with
 // nt loads+stores against 5.9 TB/s with default-policy accesses.
+// lane i <- lane i - 1 of the wave, lane 0 <- fill: one DPP wave_shr:1 move
+// (__shfl_up(v, 1) compiles to an LDS ds_bpermute round trip)
+MC_DEV uint32_t mc_wave_shr1(uint32_t x, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x138, 0xF, 0xF, false);
+}
+
 template <bool NT>
 MC_DEV mc_u32x4 mc_ld16(const void *p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const mc_u32x4 *>(p));

@@ -341,11 +341,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__re
 #pragma unroll
   for (int r = 0; r < DE_V; ++r) {
     const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
-    uint32_t p_hi = __shfl_up(x[r].w, 1, 64), p_lo = __shfl_up(x[r].z, 1, 64);
-    if (lane == 0) {
-      p_hi = q_hi[r];
-      p_lo = q_lo[r];
-    }
+    // the previous 8 bytes: lane - 1's last dwords, lane 0's read above
+    const uint32_t p_hi = mc_wave_shr1(x[r].w, q_hi[r]), p_lo = mc_wave_shr1(x[r].z, q_lo[r]);
     const mc_u32x4 y = delta_vec<ES>(x[r], p_lo, p_hi);
     if (off + 16 <= nbytes) {
       mc_st16<true>(dst + off, y);
