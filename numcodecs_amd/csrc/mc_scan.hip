@@ -1086,6 +1086,32 @@ MC_DEV void fs_store(uint8_t *dst, size_t n, size_t t0, const typename FsT<A_, D
 // p[q][e] = the tile-relative inclusive prefix sum (double) of this thread's
 // element e of segment q.  Fixed association (element, lane, wave, segment
 // order), so the reduce and apply passes compute bitwise the same values.
+// Wave-wide inclusive scan of one double per lane by DPP moves (row_shr 1, 2,
+// 4, 8 inside each row of 16 lanes, then row_bcast 15 / 31 across rows):
+// 12 v_mov_dpp + 6 adds, no LDS (the __shfl_up Hillis-Steele scan is 12
+// ds_bpermute round trips).  Lanes without a source add -0.0, the exact
+// identity (x + -0.0 == x bitwise for every x but a signalling NaN, and the
+// speculative scan treats non-finite values as failures anyway).
+template <int CTRL, int ROW_MASK>
+MC_DEV double mc_dpp_f64(double x) {
+  const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)xb, CTRL, ROW_MASK, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)0x80000000u, (int)(uint32_t)(xb >> 32), CTRL,
+                                                            ROW_MASK, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+MC_DEV double mc_wave_scan_f64(double x) {
+  x = x + mc_dpp_f64<0x111, 0xF>(x);  // row_shr:1
+  x = x + mc_dpp_f64<0x112, 0xF>(x);  // row_shr:2
+  x = x + mc_dpp_f64<0x114, 0xF>(x);  // row_shr:4
+  x = x + mc_dpp_f64<0x118, 0xF>(x);  // row_shr:8
+  x = x + mc_dpp_f64<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x = x + mc_dpp_f64<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+// lane i <- lane i - 1 (lane 0 <- -0.0)
+MC_DEV double mc_wave_shr1_f64(double x) { return mc_dpp_f64<0x138, 0xF>(x); }
+
 template <typename V, int W>
 MC_DEV void fs_tile_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double (&lds)[FS_Q][MC_BLOCK / 64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1098,18 +1124,12 @@ MC_DEV void fs_tile_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double (&l
     incl[q] = p[q][W - 1];
   }
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
-      const double o = __shfl_up(incl[q], off, 64);
-      if (lane >= off) incl[q] = o + incl[q];
-    }
-  }
+  for (int q = 0; q < FS_Q; ++q) incl[q] = mc_wave_scan_f64(incl[q]);
   double ex[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
     if (lane == 63) lds[q][wave] = incl[q];
-    ex[q] = __shfl_up(incl[q], 1, 64);
+    ex[q] = mc_wave_shr1_f64(incl[q]);
   }
   __syncthreads();
   double base = 0.0;
@@ -1500,13 +1520,8 @@ MC_DEV void fsw_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double *ldsq) 
     p[q][0] = (double)v[q][0];
 #pragma unroll
     for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (double)v[q][e];
-    double incl = p[q][W - 1];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double o = __shfl_up(incl, off, 64);
-      if (lane >= off) incl = o + incl;
-    }
-    const double ex = __shfl_up(incl, 1, 64);
+    const double incl = mc_wave_scan_f64(p[q][W - 1]);
+    const double ex = mc_wave_shr1_f64(incl);
     const double pre = base + (lane ? ex : 0.0);
 #pragma unroll
     for (int e = 0; e < W; ++e) p[q][e] = pre + p[q][e];
