@@ -1574,19 +1574,42 @@ MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_
   constexpr int TE = (int)fs_tile<D>();
   constexpr int NV = TE / W;  // vectors per tile
   const int wave = threadIdx.x >> 6;
+  // the I/O waves issue FSW_IOV vector loads before the first use (one at a
+  // time, each waited for, the next tile's 16 KiB took longer than the
+  // chain's tile and the chain lane idled at the barrier: noise-like data
+  // ran 4-9 % slower than k_scan_serial)
+  constexpr int FSW_IOV = 8;
   auto io_load = [&](size_t t, V *buf, int from, int step) {
     const size_t t0 = t * (size_t)TE;
-    for (int k = from; k < NV; k += step) {
-      const size_t e0 = t0 + (size_t)k * W;
-      if constexpr (A_ == D) {
-        if (e0 + W <= n) {
-          const typename Tr::svec x =
-              __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(S)));
+    if constexpr (A_ == D) {
+      for (int k0 = from; k0 < NV; k0 += FSW_IOV * step) {
+        typename Tr::svec xv[FSW_IOV];
 #pragma unroll
-          for (int e = 0; e < W; ++e) buf[k * W + e] = (V)x[e];
-          continue;
+        for (int u = 0; u < FSW_IOV; ++u) {
+          const int k = k0 + u * step;
+          const size_t e0 = t0 + (size_t)k * W;
+          if (k < NV && e0 + W <= n)
+            xv[u] = __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(S)));
+        }
+#pragma unroll
+        for (int u = 0; u < FSW_IOV; ++u) {
+          const int k = k0 + u * step;
+          const size_t e0 = t0 + (size_t)k * W;
+          if (k >= NV) continue;
+          if (e0 + W <= n) {
+#pragma unroll
+            for (int e = 0; e < W; ++e) buf[k * W + e] = (V)xv[u][e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+              buf[k * W + e] = e0 + e < n ? Tr::from_bits(mc_load_elem_u(src, e0 + e, sizeof(S)), a) : (V)0;
+          }
         }
       }
+      return;
+    }
+    for (int k = from; k < NV; k += step) {
+      const size_t e0 = t0 + (size_t)k * W;
       const int as = mc_itemsize(a);
 #pragma unroll
       for (int e = 0; e < W; ++e)
