@@ -295,6 +295,50 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_enc_pair(
   }
 }
 
+// ---------------------------------------------------------------------------
+// es = 4 with 16-B plane stores (V_WIDE, lab): a thread owns groups of 4
+// consecutive quads (16 elements, 64 B), loaded as 4 16-B vectors at a 64-B
+// lane stride (the 4 load instructions of a group cover 16 KiB of the wave's
+// tile contiguously between them); the 4 quads' plane dwords of plane b are
+// 16 consecutive plane bytes, so every plane store is 16 B per lane, 1 KiB
+// contiguous per wave instruction.  Same tiles as k_shuffle_enc<4, QMUL>.
+// ---------------------------------------------------------------------------
+template <bool BITROUND, bool NT, int QMUL>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_enc_wide(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
+    McBitRound br) {
+  using G = Geom<4, QMUL>;
+  static_assert(G::Q == 4 * QMUL, "4 quads per group");
+  const int tid = threadIdx.x;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)G::TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)G::TE;
+    uint32_t w[QMUL][4][4];
+#pragma unroll
+    for (int g = 0; g < QMUL; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) load_quad<4, NT>(s + (size_t)(g * MC_BLOCK + tid) * 64 + 16 * j, w[g][j]);
+#pragma unroll
+    for (int g = 0; g < QMUL; ++g) {
+      uint32_t pl[4][4];  // [plane][quad]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (BITROUND) mc_bitround_quad<4>(w[g][j], br);
+        uint32_t p[4];
+        mc_quad_to_planes<4>(w[g][j], p);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) pl[b][j] = p[b];
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        mc_st16<NT>(d + (size_t)b * m.count + (size_t)(g * MC_BLOCK + tid) * 16,
+                    mc_u32x4{pl[b][0], pl[b][1], pl[b][2], pl[b][3]});
+    }
+  }
+}
+
 template <bool NT, int QMUL>
 __global__ __launch_bounds__(MC_BLOCK) void k_shuffle4_dec_pair(
     const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles) {
@@ -477,7 +521,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec_generic(
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4, V_PAIR = 5 };
+enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4, V_PAIR = 5, V_WIDE = 6 };
 // variant | V_NO_NT selects default-policy (temporal) global accesses
 static constexpr int V_NO_NT = 8;
 // variant | V_BIG selects 2x larger tiles, | V_BIG4 4x (register layout only)
@@ -517,6 +561,12 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
                           size_t ntiles, unsigned grid, const McBitRound &br, hipStream_t st) {
   using G = Geom<ES>;
   if constexpr (ES == 4) {
+    if ((layout & 7) == V_WIDE) {
+      if (layout & V_BIG4) k_shuffle4_enc_wide<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG) k_shuffle4_enc_wide<BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else k_shuffle4_enc_wide<BR, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      return;
+    }
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG4) k_shuffle4_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else if (layout & V_BIG) k_shuffle4_enc_pair<BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
@@ -555,8 +605,9 @@ static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
                             size_t ntiles, unsigned grid, const McBitRound &br,
                             hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
-  if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
+  if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
+  if ((layout & 7) == V_WIDE && (ES != 4 || (layout & V_PIPE))) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
   else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
   return mc_last_launch();
@@ -612,7 +663,7 @@ static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
 }
 
 static size_t tile_elems(size_t es, int variant) {
-  if ((variant & 7) == V_PAIR && es == 4)  // Geom<4, QMUL> tiles
+  if (((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) && es == 4)  // Geom<4, QMUL> tiles
     return (variant & V_BIG4) ? 16384 : (variant & V_BIG) ? 8192 : 4096;
   if ((variant & 7) == V_PAIR)  // 256 lanes x NV 16-B units of 8-B elements
     return (variant & V_BIG4) ? 8192 : (variant & V_BIG) ? 4096 : 2048;
@@ -665,8 +716,10 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   const McBitRound &brr = br ? *br : nobr;
   if ((variant & 7) != V_GENERIC) {
     if ((variant & 7) == V_PAIR && es != 8 && es != 4) variant = V_REG | (variant & V_NO_NT);
-    if ((variant & 7) != V_REG && (variant & 7) != V_PAIR) variant &= ~(V_BIG | V_BIG4 | V_PIPE);
-    if ((variant & 7) == V_PAIR) variant &= ~V_PIPE;
+    if ((variant & 7) == V_WIDE && (es != 4 || !enc)) variant = V_REG | (variant & V_NO_NT);
+    if ((variant & 7) != V_REG && (variant & 7) != V_PAIR && (variant & 7) != V_WIDE)
+      variant &= ~(V_BIG | V_BIG4 | V_PIPE);
+    if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) variant &= ~V_PIPE;
     if (variant & V_PIPE) variant &= ~V_GROUP_MASK;
     if (variant & V_BIG4) variant &= ~V_BIG;
     m.group = 1u << ((variant & V_GROUP_MASK) >> V_GROUP_SHIFT);

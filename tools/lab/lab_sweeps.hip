@@ -45,7 +45,7 @@ int mc_lab_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype,
 // | 256 software-pipelined persistent loop; max_blocks 0 = default grid.
 int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize, int encode,
                            int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > 5 || (variant & ~0x1FF) != 0) return MC_EINVAL;
+  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x1FF) != 0) return MC_EINVAL;
   return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
                          (hipStream_t)stream);
 }
