@@ -39,7 +39,7 @@ def test_shuffle_every_variant(device, es):
     without a tail, through the tuning entry point."""
     st = torch.cuda.current_stream().cuda_stream
     lib = lab_lib()
-    variants = [1, 2, 3, 4, 9, 10, 11, 17, 129, 33, 65, 257, 273, 385, 5, 21, 133]
+    variants = [1, 2, 3, 4, 9, 10, 11, 17, 129, 33, 65, 257, 273, 385, 5, 21, 133, 6, 22, 134]
     for count in (4096 * 16 + 64, 16384 * 8, 4096 * 3 + 4):
         n = es * count
         x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=device)
