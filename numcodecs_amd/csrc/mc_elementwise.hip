@@ -75,14 +75,15 @@ __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ sr
     return mc_num_to_bits(map_op<KIND>(mc_num_from_bits(e, d), d, t1, t2, a, prm.s0, prm.s1, prm.rcp, prm.fastdiv), a);
   };
   if (VEC && base + ELEMS_PER_BLOCK <= n) {
-    // whole block in range: every load of the block issued before any store
+    // whole block in range: every load of the block issued before any store;
+    // nontemporal accesses (streamed once)
     constexpr int NS = EPL == 2 ? 2 * STEPS : STEPS;
     uint64_t e[NS][EPL];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const size_t i0 = base + (size_t)s * EPL * MC_BLOCK + EPL * (size_t)threadIdx.x;
-      if constexpr (EPL == 2) mc_load2(src + i0 * ss, ss, e[s]);
-      else mc_load4(src + i0 * ss, ss, e[s]);
+      if constexpr (EPL == 2) mc_load2<true>(src + i0 * ss, ss, e[s]);
+      else mc_load4<true>(src + i0 * ss, ss, e[s]);
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -90,8 +91,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_map(const uint8_t *__restrict__ sr
       uint64_t o[EPL];
 #pragma unroll
       for (int k = 0; k < EPL; ++k) o[k] = op(e[s][k]);
-      if constexpr (EPL == 2) mc_store2(dst + i0 * ds, ds, o);
-      else mc_store4(dst + i0 * ds, ds, o);
+      if constexpr (EPL == 2) mc_store2<true>(dst + i0 * ds, ds, o);
+      else mc_store4<true>(dst + i0 * ds, ds, o);
     }
     return;
   }

@@ -192,28 +192,30 @@ MC_DEV void mc_store_elem_u(uint8_t *p, size_t idx, int size, uint64_t v) {
 }
 
 // 4 consecutive elements (4*size bytes, 4*size-aligned) as one vector access
+template <bool NT = false>
 MC_DEV void mc_load4(const uint8_t *p, int size, uint64_t (&e)[4]) {
   switch (size) {
     case 1: {
-      const uint32_t w = mc_ld4<false>(p);
+      const uint32_t w = mc_ld4<NT>(p);
       for (int k = 0; k < 4; ++k) e[k] = (w >> (8 * k)) & 0xffu;
     } break;
     case 2: {
-      const mc_u32x2 w = mc_ld8<false>(p);
+      const mc_u32x2 w = mc_ld8<NT>(p);
       e[0] = w.x & 0xffffu; e[1] = w.x >> 16; e[2] = w.y & 0xffffu; e[3] = w.y >> 16;
     } break;
     case 4: {
-      const mc_u32x4 w = mc_ld16<false>(p);
+      const mc_u32x4 w = mc_ld16<NT>(p);
       e[0] = w.x; e[1] = w.y; e[2] = w.z; e[3] = w.w;
     } break;
     default: {
-      const mc_u32x4 a = mc_ld16<false>(p), b = mc_ld16<false>(p + 16);
+      const mc_u32x4 a = mc_ld16<NT>(p), b = mc_ld16<NT>(p + 16);
       e[0] = ((uint64_t)a.y << 32) | a.x; e[1] = ((uint64_t)a.w << 32) | a.z;
       e[2] = ((uint64_t)b.y << 32) | b.x; e[3] = ((uint64_t)b.w << 32) | b.z;
     } break;
   }
 }
 // 2 consecutive elements (2*size bytes, 2*size-aligned) as one vector access
+template <bool NT = false>
 MC_DEV void mc_load2(const uint8_t *p, int size, uint64_t (&e)[2]) {
   switch (size) {
     case 1: {
@@ -221,47 +223,49 @@ MC_DEV void mc_load2(const uint8_t *p, int size, uint64_t (&e)[2]) {
       e[0] = w & 0xffu; e[1] = w >> 8;
     } break;
     case 2: {
-      const uint32_t w = mc_ld4<false>(p);
+      const uint32_t w = mc_ld4<NT>(p);
       e[0] = w & 0xffffu; e[1] = w >> 16;
     } break;
     case 4: {
-      const mc_u32x2 w = mc_ld8<false>(p);
+      const mc_u32x2 w = mc_ld8<NT>(p);
       e[0] = w.x; e[1] = w.y;
     } break;
     default: {
-      const mc_u32x4 a = mc_ld16<false>(p);
+      const mc_u32x4 a = mc_ld16<NT>(p);
       e[0] = ((uint64_t)a.y << 32) | a.x; e[1] = ((uint64_t)a.w << 32) | a.z;
     } break;
   }
 }
+template <bool NT = false>
 MC_DEV void mc_store2(uint8_t *p, int size, const uint64_t (&e)[2]) {
   switch (size) {
     case 1: *reinterpret_cast<uint16_t *>(p) = (uint16_t)((e[0] & 0xff) | ((e[1] & 0xff) << 8)); break;
-    case 2: mc_st4<false>(p, (uint32_t)((e[0] & 0xffff) | ((e[1] & 0xffff) << 16))); break;
-    case 4: mc_st8<false>(p, mc_u32x2{(uint32_t)e[0], (uint32_t)e[1]}); break;
+    case 2: mc_st4<NT>(p, (uint32_t)((e[0] & 0xffff) | ((e[1] & 0xffff) << 16))); break;
+    case 4: mc_st8<NT>(p, mc_u32x2{(uint32_t)e[0], (uint32_t)e[1]}); break;
     default:
-      mc_st16<false>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1], (uint32_t)(e[1] >> 32)});
+      mc_st16<NT>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1], (uint32_t)(e[1] >> 32)});
       break;
   }
 }
 
+template <bool NT = false>
 MC_DEV void mc_store4(uint8_t *p, int size, const uint64_t (&e)[4]) {
   switch (size) {
     case 1:
-      mc_st4<false>(p, (uint32_t)((e[0] & 0xff) | ((e[1] & 0xff) << 8) | ((e[2] & 0xff) << 16) |
+      mc_st4<NT>(p, (uint32_t)((e[0] & 0xff) | ((e[1] & 0xff) << 8) | ((e[2] & 0xff) << 16) |
                                   ((e[3] & 0xff) << 24)));
       break;
     case 2:
-      mc_st8<false>(p, mc_u32x2{(uint32_t)((e[0] & 0xffff) | ((e[1] & 0xffff) << 16)),
+      mc_st8<NT>(p, mc_u32x2{(uint32_t)((e[0] & 0xffff) | ((e[1] & 0xffff) << 16)),
                                 (uint32_t)((e[2] & 0xffff) | ((e[3] & 0xffff) << 16))});
       break;
     case 4:
-      mc_st16<false>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)e[1], (uint32_t)e[2], (uint32_t)e[3]});
+      mc_st16<NT>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)e[1], (uint32_t)e[2], (uint32_t)e[3]});
       break;
     default:
-      mc_st16<false>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1],
+      mc_st16<NT>(p, mc_u32x4{(uint32_t)e[0], (uint32_t)(e[0] >> 32), (uint32_t)e[1],
                                  (uint32_t)(e[1] >> 32)});
-      mc_st16<false>(p + 16, mc_u32x4{(uint32_t)e[2], (uint32_t)(e[2] >> 32), (uint32_t)e[3],
+      mc_st16<NT>(p + 16, mc_u32x4{(uint32_t)e[2], (uint32_t)(e[2] >> 32), (uint32_t)e[3],
                                       (uint32_t)(e[3] >> 32)});
       break;
   }
