@@ -350,11 +350,14 @@ inline unsigned ck_grid_cap(bool copy, bool crc) {
   return crc ? 0xffffffffu : 2048u;
 }
 
-// the bit-sliced CRC kernel's persistent grid (two workgroups per CU at its
-// register budget): ck_grid / ck_grid_copy when set, else 512
+// the bit-sliced CRC kernel's grid: ck_grid / ck_grid_copy when set, else
+// 2048 workgroups for the checksum-only passes (two resident per CU, so four
+// rounds of two tiles each: 1-2 us faster than one round of 512 persistent
+// workgroups for the 256 MiB verify, profiles/r03/probe_crc_bs.jsonl) and the
+// copy passes' 1024
 inline unsigned ck_grid_cap_bs(bool copy) {
   const int g = copy ? mc_sched.ck_grid_copy : mc_sched.ck_grid;
-  return g > 0 ? (unsigned)g : 512u;
+  return g > 0 ? (unsigned)g : 2048u;
 }
 
 // tile size (in STEP units) for a chunk: K = 1 below 64 KiB
