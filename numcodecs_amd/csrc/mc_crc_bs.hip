@@ -5,11 +5,12 @@
 
 namespace mcck {
 // ---------------------------------------------------------------------------
-// CRC tiles with the bit-sliced fold (crc_fold_bs, K >= 4): no LDS tables, a
-// persistent grid, and the next tile's K vectors loaded into a second
-// register set before the current tile is folded (the fold is ~3 VALU ops
-// per byte, so with one tile per workgroup the loads and the XOR network of
-// a workgroup serialise and ~half the wave time waited on memory).  Lane
+// CRC tiles with the bit-sliced fold (crc_fold_bs, K >= 4): no LDS tables;
+// workgroups loop over tiles (grid: ck_grid_cap_bs) with the next tile's K
+// vectors loaded into a second register set before the current tile is
+// folded (the fold is ~3 VALU ops per byte, so with one tile per workgroup
+// the loads and the XOR network of a workgroup serialise and ~half the wave
+// time waited on memory).  Lane
 // alignment x^(-128 l) uses the 32 products g * x^i kept in registers (one
 // v_bitop3 + one v_bfe per bit); the four wave partials of a tile go through
 // a parity-double-buffered LDS slot, one barrier per tile.
