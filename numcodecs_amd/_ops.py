@@ -537,6 +537,30 @@ def packbits(src, dst, n) -> None:
         check(lib.mc_packbits(src.data_ptr() if n else None, dst.data_ptr(), n, stream(dst)), "mc_packbits")
 
 
+def unpackbits_device(src, src_bytes):
+    """PackBits.decode of a device buffer without a host round trip before
+    the launch: the padding byte is copied to pinned memory ahead of the
+    kernel on the same stream, the kernel unpacks all 8 * (src_bytes - 1)
+    bits (at most 7 past the end: the returned view drops them), and the
+    host waits only for the 1-byte copy.  Returns the uint8 tensor of bools,
+    or None when the stream is being captured into a graph."""
+    _native.require_device()
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    nmax = 8 * (src_bytes - 1)
+    with _guard(src):
+        dst = torch.empty(max(nmax, 1), dtype=torch.uint8, device=src.device)
+        pad_h = torch.empty(1, dtype=torch.uint8, pin_memory=True)
+        pad_h.copy_(src[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        if nmax:
+            check(lib.mc_unpackbits(src.data_ptr(), src_bytes, dst.data_ptr(), nmax, stream(src)), "mc_unpackbits")
+        ev.synchronize()
+        n = max(nmax - int(pad_h[0]), 0)
+    return dst[:n]
+
+
 def unpackbits(src, src_bytes, dst, n) -> None:
     _native.require_device()
     if n == 0:

@@ -36,6 +36,10 @@ class PackBits(Codec):
         nb = src.nbytes
         if nb == 0:  # enc[0] of an empty array
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+        if not src.host:
+            dst = _ops.unpackbits_device(src.data, nb)
+            if dst is not None:
+                return ndarray_copy(dst.view(torch.bool), out)
         pad = int(download(src.data[:1])[0])
         n = max(8 * (nb - 1) - pad, 0)
         dst = empty_like_bytes(n, src)
