@@ -1004,15 +1004,19 @@ struct FsT {
     if constexpr (sizeof(S) == 8) return __builtin_isfinite(c);
     else return __builtin_isfinite((float)c);
   }
-  // the candidate of lane - 1 (bit pattern moved through an integer shuffle)
+  // the candidate of lane - 1 (lane 0 keeps its own, as __shfl_up(c, 1)
+  // would): the bit pattern moved by DPP wave_shr:1, no LDS round trip
   MC_DEV static S shfl_up1(S c) {
     if constexpr (sizeof(S) == 8) {
-      return __builtin_bit_cast(S, (unsigned long long)__shfl_up(__builtin_bit_cast(unsigned long long, c), 1, 64));
+      const uint64_t b = __builtin_bit_cast(uint64_t, c);
+      const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+      return __builtin_bit_cast(S, ((uint64_t)mc_wave_shr1(hi, hi) << 32) | mc_wave_shr1(lo, lo));
     } else if constexpr (sizeof(S) == 4) {
-      return __builtin_bit_cast(S, (unsigned int)__shfl_up(__builtin_bit_cast(unsigned int, c), 1, 64));
+      const uint32_t b = __builtin_bit_cast(uint32_t, c);
+      return __builtin_bit_cast(S, mc_wave_shr1(b, b));
     } else {
-      const unsigned int b = __shfl_up((unsigned int)__builtin_bit_cast(uint16_t, c), 1, 64);
-      return __builtin_bit_cast(S, (uint16_t)b);
+      const uint32_t b = __builtin_bit_cast(uint16_t, c);
+      return __builtin_bit_cast(S, (uint16_t)mc_wave_shr1(b, b));
     }
   }
 };
