@@ -254,6 +254,110 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
 }
 
 // ---------------------------------------------------------------------------
+// es = 8 with lane quads (V_WIDE, lab): lanes 4m..4m+3 hold elements
+// 8m..8m+7 (2 each, 16 B, lane-contiguous as in the pair layout) and lane j
+// of the quad owns planes j and j+4 of all 8 elements, so each plane access
+// is 8 B per lane instead of the pair layout's 4 B.  The exchange is a 4x4
+// all-to-all of dwords inside the quad: a byte transpose builds, per
+// destination lane, the dword of that lane's plane bytes, then two DPP
+// butterflies (quad_perm xor 1, xor 2; no LDS) deliver them.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+MC_DEV uint32_t mc_quad_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+// a[k] is destined to quad lane k; on return q[s] is what quad lane s sent here
+MC_DEV void mc_quad_a2a(const uint32_t (&a)[4], uint32_t (&q)[4], int j) {
+  const bool b0 = j & 1, b1 = j & 2;
+  // xor 1: keep the items for lanes with my bit 0, trade the others
+  const uint32_t r0 = mc_quad_dpp<0xB1>(b0 ? a[0] : a[1]);
+  const uint32_t r1 = mc_quad_dpp<0xB1>(b0 ? a[2] : a[3]);
+  // (from the even, from the odd lane of my pair) for destinations j&1 and (j&1)+2
+  const uint32_t e_lo = b0 ? r0 : a[0], o_lo = b0 ? a[1] : r0;
+  const uint32_t e_hi = b0 ? r1 : a[2], o_hi = b0 ? a[3] : r1;
+  // xor 2: keep the destination with my bit 1, trade the other
+  const uint32_t u0 = mc_quad_dpp<0x4E>(b1 ? e_lo : e_hi);
+  const uint32_t u1 = mc_quad_dpp<0x4E>(b1 ? o_lo : o_hi);
+  q[0] = b1 ? u0 : e_lo;
+  q[1] = b1 ? u1 : o_lo;
+  q[2] = b1 ? e_hi : u0;
+  q[3] = b1 ? o_hi : u1;
+}
+
+template <bool BITROUND, bool NT, int NV>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_quad(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
+    McBitRound br) {
+  constexpr int TB = NV * 16 * MC_BLOCK, TE = TB / 8;
+  const int tid = threadIdx.x, j = tid & 3;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)TE;
+    mc_u32x4 v[NV];
+#pragma unroll
+    for (int r = 0; r < NV; ++r) v[r] = mc_ld16<NT>(s + ((size_t)r * MC_BLOCK + tid) * 16);
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      mc_u32x4 x = v[r];
+      if constexpr (BITROUND) {
+        uint64_t e0 = mc_bitround64(((uint64_t)x.y << 32) | x.x, br);
+        uint64_t e1 = mc_bitround64(((uint64_t)x.w << 32) | x.z, br);
+        x = mc_u32x4{(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32)};
+      }
+      // a[k] = byte k of (lo e0, lo e1, hi e0, hi e1): quad lane k's planes k, k+4
+      uint32_t a[4], q[4];
+      mc_tr4(x.x, x.z, x.y, x.w, a[0], a[1], a[2], a[3]);
+      mc_quad_a2a(a, q, j);
+      // q[s] = (plane j of elements 2s, 2s+1 | plane j+4 of the same two)
+      const uint32_t l0 = mc_perm(q[1], q[0], 0x05040100u), l1 = mc_perm(q[3], q[2], 0x05040100u);
+      const uint32_t h0 = mc_perm(q[1], q[0], 0x07060302u), h1 = mc_perm(q[3], q[2], 0x07060302u);
+      const size_t e = (size_t)r * (16 * MC_BLOCK / 8) + 8 * (size_t)(tid >> 2);
+      uint8_t *pd = d + (size_t)j * m.count + e;
+      mc_st8<NT>(pd, mc_u32x2{l0, l1});
+      mc_st8<NT>(pd + 4 * m.count, mc_u32x2{h0, h1});
+    }
+  }
+}
+
+template <bool NT, int NV>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_quad(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles) {
+  constexpr int TB = NV * 16 * MC_BLOCK, TE = TB / 8;
+  const int tid = threadIdx.x, j = tid & 3;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)TE;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)TB;
+    mc_u32x2 lo[NV], hi[NV];
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      const size_t e = (size_t)r * (16 * MC_BLOCK / 8) + 8 * (size_t)(tid >> 2);
+      const uint8_t *ps = s + (size_t)j * m.count + e;
+      lo[r] = mc_ld8<NT>(ps);
+      hi[r] = mc_ld8<NT>(ps + 4 * m.count);
+    }
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      // a[s] = (plane j | plane j+4 bytes of elements 2s, 2s+1): quad lane s's
+      uint32_t a[4], q[4];
+      a[0] = mc_perm(hi[r].x, lo[r].x, 0x05040100u);
+      a[1] = mc_perm(hi[r].x, lo[r].x, 0x07060302u);
+      a[2] = mc_perm(hi[r].y, lo[r].y, 0x05040100u);
+      a[3] = mc_perm(hi[r].y, lo[r].y, 0x07060302u);
+      mc_quad_a2a(a, q, j);
+      // q[k] = byte k of (lo e0, lo e1, hi e0, hi e1) of my two elements
+      uint32_t lo0, lo1, hi0, hi1;
+      mc_tr4(q[0], q[1], q[2], q[3], lo0, lo1, hi0, hi1);
+      mc_st16<NT>(d + ((size_t)r * MC_BLOCK + tid) * 16, mc_u32x4{lo0, hi0, lo1, hi1});
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // es = 4 with lane pairs on the plane side: lanes 2j and 2j+1 hold the quads
 // of 8 consecutive elements; one DPP pair swap (quad_perm [1,0,3,2], no LDS)
 // of two plane dwords lets the even lane own planes 0-1 and the odd lane
@@ -575,6 +679,12 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     }
   }
   if constexpr (ES == 8) {
+    if ((layout & 7) == V_WIDE) {
+      if (layout & V_BIG4) k_shuffle8_enc_quad<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG) k_shuffle8_enc_quad<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else k_shuffle8_enc_quad<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      return;
+    }
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else if (layout & V_BIG) k_shuffle8_enc_pair<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
@@ -607,7 +717,7 @@ static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
   if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
-  if ((layout & 7) == V_WIDE && (ES != 4 || (layout & V_PIPE))) return MC_EINVAL;
+  if ((layout & 7) == V_WIDE && ((ES != 4 && ES != 8) || (layout & V_PIPE))) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
   else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
   return mc_last_launch();
@@ -626,6 +736,12 @@ static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     }
   }
   if constexpr (ES == 8) {
+    if ((layout & 7) == V_WIDE) {
+      if (layout & V_BIG4) k_shuffle8_dec_quad<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else if (layout & V_BIG) k_shuffle8_dec_quad<NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else k_shuffle8_dec_quad<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      return;
+    }
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG4) k_shuffle8_dec_pair<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       else if (layout & V_BIG) k_shuffle8_dec_pair<NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
@@ -655,8 +771,9 @@ template <int ES>
 static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                             size_t ntiles, unsigned grid, hipStream_t st) {
   const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
-  if ((layout & 7) < V_REG || (layout & 7) > V_PAIR || (layout & 7) == V_GENERIC) return MC_EINVAL;
+  if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
+  if ((layout & 7) == V_WIDE && (ES != 8 || (layout & V_PIPE))) return MC_EINVAL;
   if (variant & V_NO_NT) launch_dec_nt<ES, false>(layout, s, d, m, ntiles, grid, st);
   else launch_dec_nt<ES, true>(layout, s, d, m, ntiles, grid, st);
   return mc_last_launch();
@@ -665,7 +782,7 @@ static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
 static size_t tile_elems(size_t es, int variant) {
   if (((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) && es == 4)  // Geom<4, QMUL> tiles
     return (variant & V_BIG4) ? 16384 : (variant & V_BIG) ? 8192 : 4096;
-  if ((variant & 7) == V_PAIR)  // 256 lanes x NV 16-B units of 8-B elements
+  if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE)  // 256 lanes x NV 16-B units of 8-B elements
     return (variant & V_BIG4) ? 8192 : (variant & V_BIG) ? 4096 : 2048;
   const size_t te = es >= 16 ? 2048 : 4096;
   if ((variant & 7) != V_REG) return te;
@@ -716,7 +833,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   const McBitRound &brr = br ? *br : nobr;
   if ((variant & 7) != V_GENERIC) {
     if ((variant & 7) == V_PAIR && es != 8 && es != 4) variant = V_REG | (variant & V_NO_NT);
-    if ((variant & 7) == V_WIDE && (es != 4 || !enc)) variant = V_REG | (variant & V_NO_NT);
+    if ((variant & 7) == V_WIDE && !(es == 8 || (es == 4 && enc))) variant = V_REG | (variant & V_NO_NT);
     if ((variant & 7) != V_REG && (variant & 7) != V_PAIR && (variant & 7) != V_WIDE)
       variant &= ~(V_BIG | V_BIG4 | V_PIPE);
     if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) variant &= ~V_PIPE;
