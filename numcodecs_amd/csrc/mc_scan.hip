@@ -1055,6 +1055,25 @@ MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, int a,
                                : (typename Tr::V)0;
       }
     }
+  } else if constexpr (A_ == MC_F4 && D == MC_F8) {
+    // f8 <- f4 (the dispatch checks 8-B alignment): one 8-B load of the
+    // thread's 2 float32 per vector, the casts in registers.  The components
+    // are copied out before the bit casts: __builtin_bit_cast of an
+    // ext_vector component reads component 0 (seen in the gfx950 assembly)
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const size_t e0 = fs_elem0<D>(t0, q);
+      if (e0 + W <= n) {
+        const mc_u32x2 x = mc_ld8<false>(src + e0 * 4);
+        const uint32_t x0 = x.x, x1 = x.y;
+        v[q][0] = (double)__builtin_bit_cast(float, x0);
+        v[q][1] = (double)__builtin_bit_cast(float, x1);
+      } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e)
+          v[q][e] = e0 + e < n ? (double)reinterpret_cast<const float *>(src)[e0 + e] : 0.0;
+      }
+    }
   } else {
     const int as = mc_itemsize(a);
 #pragma unroll
@@ -2018,6 +2037,7 @@ static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws
 static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int dt, void *ws, hipStream_t st) {
   if (dt == MC_F8) {
     if (a == MC_F8) launch_fspec<MC_F8, MC_F8>(s, d, n, a, ws, st);
+    else if (a == MC_F4 && (uintptr_t)s % 8 == 0) launch_fspec<MC_F4, MC_F8>(s, d, n, a, ws, st);
     else launch_fspec<-1, MC_F8>(s, d, n, a, ws, st);
   } else if (dt == MC_F4) {
     if (a == MC_F4) launch_fspec<MC_F4, MC_F4>(s, d, n, a, ws, st);
@@ -2042,6 +2062,8 @@ static void launch_fspec_rows_any(const uint8_t *sc, size_t ss, uint8_t *dc, siz
                                   uint64_t *fail, unsigned g, hipStream_t st) {
   if (dt == MC_F8) {
     if (a == MC_F8) launch_fspec_rows<MC_F8, MC_F8>(sc, ss, dc, ds, n, a, fail, g, st);
+    else if (a == MC_F4 && (uintptr_t)sc % 8 == 0 && ss % 8 == 0)
+      launch_fspec_rows<MC_F4, MC_F8>(sc, ss, dc, ds, n, a, fail, g, st);
     else launch_fspec_rows<-1, MC_F8>(sc, ss, dc, ds, n, a, fail, g, st);
   } else if (dt == MC_F4) {
     if (a == MC_F4) launch_fspec_rows<MC_F4, MC_F4>(sc, ss, dc, ds, n, a, fail, g, st);
