@@ -108,7 +108,9 @@ def _run(buf, typesize, blocksize, mode, forward, clevel, cname):
         raise ValueError(f"Cannot use typesize {typesize} less than 1.")
     mode = _resolve(mode, typesize)
     src = to_dbuf(buf)
-    if blocksize is None or blocksize == AUTOBLOCKS:  # c-blosc's choice (numcodecs' default)
+    if blocksize is None:  # one block covering the whole buffer
+        blocksize = max(src.nbytes, 1)
+    elif blocksize == AUTOBLOCKS:  # c-blosc's choice (numcodecs' default)
         blocksize = max(compute_blocksize(src.nbytes, typesize, clevel, cname), 1)
     if blocksize < 1:
         raise ValueError("blocksize must be >= 1")
@@ -128,7 +130,8 @@ def shuffle(buf, typesize=None, blocksize=AUTOBLOCKS, mode=SHUFFLE, clevel=5, cn
     defaults to the buffer's itemsize; blocksize to c-blosc's automatic
     choice for `clevel` / `cname` (numcodecs' Blosc defaults: lz4, 5), which
     is what a decoder reads back from the frame header.  An explicit
-    blocksize is used exactly as given (the frame header's value)."""
+    blocksize is used exactly as given (the frame header's value); None
+    filters the whole buffer as one block."""
     return _run(buf, typesize, blocksize, mode, True, clevel, cname)
 
 

@@ -56,27 +56,32 @@ static inline uint64_t mc_now_ns() {
 
 // Spin on the verdict word for at most MC_VERDICT_SPIN_NS (a lone verify of
 // 256 MiB is ~45 us, so the usual call never leaves the spin); a verify queued
-// behind a lot of earlier work blocks in hipStreamSynchronize instead of
-// holding a host core at 100 % for as long as the stream takes.
+// behind a lot of earlier work then keeps polling with a sleep between polls
+// instead of holding a host core at 100 % for as long as the stream takes.
+// (No hipStreamSynchronize: on the legacy default stream that would also wait
+// for every other blocking stream's work, not just the verify.)
 #define MC_VERDICT_SPIN_NS 100000ull
+#define MC_VERDICT_SLEEP_NS 20000l
 
 int mc_verdict_wait(const uint32_t *rec, uint32_t seq, mc_stream_t stream) {
   if (!rec || !seq) return MC_EINVAL;
   const uint64_t t0 = mc_now_ns();
+  bool sleeping = false;
   for (unsigned i = 1;; ++i) {
     if (__atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq) return MC_OK;
-    if ((i & 1023u) == 0) {  // every ~10-20 us: has the stream ended or failed?
+    if (sleeping || (i & 1023u) == 0) {  // every ~10-20 us: has the stream ended or failed?
       const hipError_t e = hipStreamQuery((hipStream_t)stream);
       if (e == hipSuccess)
         return __atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq ? MC_OK : MC_EPROTO;
       if (e != hipErrorNotReady) return mc_hip_status(e);
-      if (mc_now_ns() - t0 > MC_VERDICT_SPIN_NS) {
-        const hipError_t s = hipStreamSynchronize((hipStream_t)stream);
-        if (s != hipSuccess) return mc_hip_status(s);
-        return __atomic_load_n(&rec[2], __ATOMIC_ACQUIRE) == seq ? MC_OK : MC_EPROTO;
-      }
+      if (!sleeping) sleeping = mc_now_ns() - t0 > MC_VERDICT_SPIN_NS;
     }
-    __builtin_ia32_pause();
+    if (sleeping) {
+      const timespec ts{0, MC_VERDICT_SLEEP_NS};
+      nanosleep(&ts, nullptr);
+    } else {
+      __builtin_ia32_pause();
+    }
   }
 }
 

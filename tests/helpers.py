@@ -104,6 +104,18 @@ def lab_lib():
     import pytest
     from lab.lablib import LAB_PATH, lab
 
+    check_lab_build()
     if not os.path.exists(LAB_PATH):  # optional: the product never needs it
         pytest.skip(f"lab library not built ({LAB_PATH}); `make -C tools/lab`")
     return lab()
+
+
+def check_lab_build():
+    """Fail (not skip) when __graft_entry__.build() recorded a failed lab build."""
+    import pytest
+
+    marker = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "_build",
+                          "LAB_BUILD_FAILED")
+    if os.path.exists(marker):
+        with open(marker) as f:
+            pytest.fail(f"the lab library failed to build: {f.read().strip()}")

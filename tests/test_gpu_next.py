@@ -367,6 +367,25 @@ def test_blosc_filters_sizes(device, mode):
             assert torch.equal(bsh.unshuffle(got, ts, bs, mode), xd), (ts, nel, bs, mode)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_blosc_filters_blocksize_none_is_one_block(device, mode):
+    """blocksize=None filters the whole buffer as ONE block (for every size,
+    also >= 32 KiB where AUTOBLOCKS would cut it); AUTOBLOCKS (0) is c-blosc's
+    choice."""
+    from numcodecs_amd import blosc_shuffle as bsh
+    from oracle import blosc
+
+    for ts, nbytes in ((4, 4096), (4, (1 << 20) + 8), (8, 3 << 20), (3, 100 * 1024 + 1)):
+        raw = RNG.integers(0, 256, nbytes, dtype=np.uint8)
+        xd = torch.from_numpy(raw).to(device)
+        got = bsh.shuffle(xd, ts, None, mode)
+        assert got.cpu().numpy().tobytes() == blosc.blosc_filter(raw, ts, nbytes, mode), (ts, nbytes, mode)
+        assert torch.equal(bsh.unshuffle(got, ts, None, mode), xd)
+        auto = bsh.compute_blocksize(nbytes, ts)
+        assert bsh.shuffle(xd, ts, bsh.AUTOBLOCKS, mode).cpu().numpy().tobytes() == \
+            blosc.blosc_filter(raw, ts, auto, mode)
+
+
 @pytest.mark.parametrize("kind_name", ["crc32", "crc32c", "adler32", "fletcher32"])
 def test_one_launch_encode_abi(device, kind_name):
     """mc_checksum32_encode_fused / mc_fletcher32_encode_fused (the payload

@@ -19,6 +19,9 @@ LAB = os.path.join(ROOT, "tools", "_build", "libmcodec_lab.so")
 
 @pytest.mark.gpu
 def test_every_lab_schedule_matches_the_oracle(device):
+    from tests.helpers import check_lab_build
+
+    check_lab_build()
     if not os.path.exists(LAB):
         pytest.skip("lab library not built (make -C tools/lab)")
     env = {k: v for k, v in os.environ.items() if not k.startswith("MCODEC_")}

@@ -24,6 +24,8 @@ _SIGS = {
     "mc_lab_c4_dec1p": ([_V, _V, _S, _I, _I, _D, _D, _V, ctypes.c_uint, _V, _V], _I),
     "mc_lab_rocprim_scan_workspace": ([_S, _I], _S),
     "mc_lab_rocprim_scan": ([_V, _V, _S, _I, _V, _S, _V], _I),
+    "mc_lab_shuffle4_enc": ([_V, _V, _S, _I, _V], _I),
+    "mc_lab_bw_copy": ([_V, _V, _S, _I, _I, _I, _V], _I),
 }
 _lib = None
 
