@@ -64,7 +64,18 @@ typedef void *mc_stream_t; /* hipStream_t */
 #define MC_ARRIVAL_WORDS 2080
 #define MC_EHIP_BASE (-1000) /* MC_EHIP_BASE - (int)hipError_t */
 
-/* dtype codes (little-endian numpy dtypes; numpy kind + itemsize) */
+/* dtype codes (numpy kind + itemsize).  A code names the little-endian
+ * (native) dtype; MC_BIG_ENDIAN OR'd into the code of a multi-byte dtype
+ * names the same dtype stored big-endian ('>i2', '>f4', ... -- numpy's
+ * non-native byte order, as Zarr v2 arrays converted from netCDF/HDF5 carry
+ * it).  Byte order only changes how an element sits in memory: the kernels
+ * reverse its bytes in registers on load / before the store and compute
+ * exactly as for the little-endian dtype (delta.py:52-83,
+ * fixedscaleoffset.py:83-113, quantize.py:60-82 and astype.py:46-58 compute
+ * big-endian arrays through numpy the same way).  Compute dtypes (the t1..t4
+ * of the FixedScaleOffset entry points) are never big-endian: numpy's
+ * arithmetic results are native. */
+#define MC_BIG_ENDIAN 32
 enum mc_dtype {
   MC_B1 = 0, /* '|b1' bool */
   MC_I1 = 1, /* '|i1' */

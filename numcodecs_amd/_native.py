@@ -45,6 +45,11 @@ DTYPE_CODES = {
     "<f4": 10,
     "<f8": 11,
 }
+# big-endian (non-native) byte order: MC_BIG_ENDIAN OR'd into the code of a
+# multi-byte dtype (include/mcodec.h); the kernels reverse each element's
+# bytes in registers (numpy normalises '>i1' / '>u1' / '>b1' to '|')
+MC_BIG_ENDIAN = 32
+DTYPE_CODES.update({">" + k[1:]: v | MC_BIG_ENDIAN for k, v in DTYPE_CODES.items() if k[0] == "<"})
 
 MC_OK = 0
 MC_EINVAL = -22

@@ -22,14 +22,15 @@ __all__ = ["dtype_code", "stream", "workspace"]
 
 
 def dtype_code(dt) -> int:
-    """mc_dtype code of numpy dtype `dt` (little-endian numeric types only)."""
+    """mc_dtype code of numpy dtype `dt`: bool/int/uint/float of either byte
+    order (a big-endian dtype carries MC_BIG_ENDIAN)."""
     dt = np.dtype(dt)
     try:
         return DTYPE_CODES[dt.str]
     except KeyError:
         raise NotImplementedError(
             f"dtype {dt.str!r} is not supported by the numcodecs_amd device kernels "
-            "(little-endian bool/int/uint/float only)"
+            "(bool/int/uint/float only)"
         ) from None
 
 

@@ -148,8 +148,14 @@ static inline unsigned mc_grid_for(size_t work_items, size_t per_block,
 // ---------------------------------------------------------------------------
 // dtype table
 // ---------------------------------------------------------------------------
+// A dtype code may carry MC_BIG_ENDIAN (include/mcodec.h): every helper below
+// answers for the dtype itself (byte order aside); mc_num_from_bits /
+// mc_num_to_bits (mc_num.h) and mc_to_storage reverse the bytes.  With a
+// compile-time code every test folds away.
+MC_HD constexpr int mc_dt_base(int dt) { return dt & ~MC_BIG_ENDIAN; }
+MC_HD constexpr bool mc_dt_swapped(int dt) { return (dt & MC_BIG_ENDIAN) != 0; }
 MC_HD int mc_itemsize(int dt) {
-  switch (dt) {
+  switch (mc_dt_base(dt)) {
     case MC_B1: case MC_I1: case MC_U1: return 1;
     case MC_I2: case MC_U2: case MC_F2: return 2;
     case MC_I4: case MC_U4: case MC_F4: return 4;
@@ -157,11 +163,53 @@ MC_HD int mc_itemsize(int dt) {
     default: return 0;
   }
 }
-MC_HD bool mc_is_float(int dt) { return dt == MC_F2 || dt == MC_F4 || dt == MC_F8; }
+MC_HD bool mc_is_float(int dt) {
+  dt = mc_dt_base(dt);
+  return dt == MC_F2 || dt == MC_F4 || dt == MC_F8;
+}
 MC_HD bool mc_is_signed(int dt) {
+  dt = mc_dt_base(dt);
   return dt == MC_I1 || dt == MC_I2 || dt == MC_I4 || dt == MC_I8;
 }
-static inline bool mc_valid_dtype(int dt) { return dt >= 0 && dt < MC_NDTYPES; }
+// a little-endian code, or a big-endian one of a multi-byte dtype
+static inline bool mc_valid_dtype(int dt) {
+  const int b = mc_dt_base(dt);
+  return b >= 0 && b < MC_NDTYPES && (dt & ~(MC_BIG_ENDIAN | 31)) == 0 &&
+         (!mc_dt_swapped(dt) || mc_itemsize(b) > 1);
+}
+// a little-endian (native) code only
+static inline bool mc_valid_native_dtype(int dt) { return dt >= 0 && dt < MC_NDTYPES; }
+
+// the low `size` bytes of v in reverse order (v_perm_b32 on the device)
+MC_HD uint64_t mc_bswap_n(uint64_t v, int size) {
+  switch (size) {
+    case 2: return __builtin_bswap16((uint16_t)v);
+    case 4: return __builtin_bswap32((uint32_t)v);
+    case 8: return __builtin_bswap64(v);
+    default: return v;
+  }
+}
+// an element's raw little-endian-assembled bits <-> its storage in dtype dt
+// (identity unless dt is big-endian); its own inverse
+MC_HD uint64_t mc_to_storage(uint64_t bits, int dt) {
+  return mc_dt_swapped(dt) ? mc_bswap_n(bits, mc_itemsize(dt)) : bits;
+}
+// byte reversal of every ES-byte element packed in a 16-B vector
+template <int ES>
+MC_DEV mc_u32x4 mc_bswap_vec(mc_u32x4 v) {
+  const uint32_t a = v.x, b = v.y, c = v.z, d = v.w;  // components copied out first
+  if constexpr (ES == 2) {
+    constexpr uint32_t S = 0x02030001u;  // bytes 1 0 3 2
+    return mc_u32x4{__builtin_amdgcn_perm(0u, a, S), __builtin_amdgcn_perm(0u, b, S),
+                    __builtin_amdgcn_perm(0u, c, S), __builtin_amdgcn_perm(0u, d, S)};
+  } else if constexpr (ES == 4) {
+    return mc_u32x4{__builtin_bswap32(a), __builtin_bswap32(b), __builtin_bswap32(c), __builtin_bswap32(d)};
+  } else if constexpr (ES == 8) {
+    return mc_u32x4{__builtin_bswap32(b), __builtin_bswap32(a), __builtin_bswap32(d), __builtin_bswap32(c)};
+  } else {
+    return v;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // byte transposes (v_perm_b32).  perm(hi, lo, sel): byte k of the result is

@@ -313,7 +313,9 @@ MC_DEV mc_u32x4 delta_vec(mc_u32x4 x, uint32_t p_lo, uint32_t p_hi) {
   }
 }
 
-template <int ES>
+// SW: bit 0 = the input is big-endian, bit 1 = the output is (the bytes of
+// each element reversed after the load / before the store, v_perm_b32)
+template <int ES, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__restrict__ src,
                                                              uint8_t *__restrict__ dst, size_t nbytes,
                                                              size_t src_stride, size_t dst_stride) {
@@ -338,13 +340,20 @@ __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__re
       q_hi[r] = *reinterpret_cast<const uint32_t *>(src + off - 4);
       if (ES == 8) q_lo[r] = *reinterpret_cast<const uint32_t *>(src + off - 8);
     }
+    if constexpr (SW & 1) {  // big-endian input: every element to register order
+      x[r] = mc_bswap_vec<ES>(x[r]);
+      const mc_u32x4 q = mc_bswap_vec<ES>(mc_u32x4{q_lo[r], q_hi[r], 0u, 0u});
+      q_lo[r] = q.x;
+      q_hi[r] = q.y;
+    }
   }
 #pragma unroll
   for (int r = 0; r < DE_V; ++r) {
     const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
     // the previous 8 bytes: lane - 1's last dwords, lane 0's read above
     const uint32_t p_hi = mc_wave_shr1(x[r].w, q_hi[r]), p_lo = mc_wave_shr1(x[r].z, q_lo[r]);
-    const mc_u32x4 y = delta_vec<ES>(x[r], p_lo, p_hi);
+    mc_u32x4 y = delta_vec<ES>(x[r], p_lo, p_hi);
+    if constexpr ((SW & 2) != 0) y = mc_bswap_vec<ES>(y);  // big-endian output
     if (off + 16 <= nbytes) {
       mc_st16<true>(dst + off, y);
     } else if (off < nbytes) {
@@ -365,30 +374,48 @@ static unsigned blocks_for(size_t n) {
   return (unsigned)((n + ELEMS_PER_BLOCK - 1) / ELEMS_PER_BLOCK);
 }
 
+// one constant-dtype instantiation per byte-order combination of the input
+// (D) and output (A) dtypes: the byte reversals fold into the loads/stores
+template <int KIND, int D, int T1, int T2, int A, int EPL = 4>
+static void launch_map_bo(bool sd, bool sa, unsigned grid, const uint8_t *s, uint8_t *d, size_t n,
+                          const MapParams &p, hipStream_t st) {
+  constexpr int BE = MC_BIG_ENDIAN;
+  if (!sd && !sa) k_map<KIND, D, T1, T2, A, true, EPL><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  else if (sd && !sa) k_map<KIND, D | BE, T1, T2, A, true, EPL><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  else if (!sd) k_map<KIND, D, T1, T2, A | BE, true, EPL><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  else k_map<KIND, D | BE, T1, T2, A | BE, true, EPL><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+}
+
 template <int KIND>
 static int launch_map(const void *src, void *dst, size_t n, const MapParams &p, hipStream_t st) {
   if (n == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;
-  if (!mc_valid_dtype(p.d) || !mc_valid_dtype(p.t1) || !mc_valid_dtype(p.t2) || !mc_valid_dtype(p.a))
+  // input / output dtypes may be big-endian; the compute dtypes never are
+  if (!mc_valid_dtype(p.d) || !mc_valid_native_dtype(p.t1) || !mc_valid_native_dtype(p.t2) ||
+      !mc_valid_dtype(p.a))
     return MC_EINVAL;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   const bool vec = aligned_for(src, mc_itemsize(p.d)) && aligned_for(dst, mc_itemsize(p.a));
   const unsigned grid = blocks_for(n);
-  // specialised hot paths (constant dtypes): C4's FSO f4 -> i2 and i2 -> f4
-  if (KIND == K_FSO_ENC && vec && p.d == MC_F4 && p.t1 == MC_F4 && p.t2 == MC_F4 && p.a == MC_I2) {
-    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_I2, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
-  } else if (KIND == K_FSO_DEC && vec && p.d == MC_I2 && p.t1 == MC_F8 && p.t2 == MC_F8 &&
-             p.a == MC_F4) {
-    k_map<KIND, MC_I2, MC_F8, MC_F8, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
-  } else if (KIND == K_QUANTIZE && vec && p.d == MC_F4 && p.a == MC_F4) {
-    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_F4, true><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
-  } else if (KIND == K_CAST && vec && p.d == MC_F4 && p.a == MC_F8) {  // AsType / Quantize decode
-    k_map<KIND, MC_F4, MC_F4, MC_F4, MC_F8, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
-  } else if (KIND == K_CAST && vec && p.d == MC_F8 && p.a == MC_F4) {
-    k_map<KIND, MC_F8, MC_F8, MC_F8, MC_F4, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
-  } else if (KIND == K_QUANTIZE && vec && p.d == MC_F8 && p.a == MC_F4) {
-    k_map<KIND, MC_F8, MC_F8, MC_F8, MC_F4, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
+  const int db = mc_dt_base(p.d), ab = mc_dt_base(p.a);
+  const bool sd = mc_dt_swapped(p.d), sa = mc_dt_swapped(p.a);
+  // specialised hot paths (constant dtypes, any byte order): C4's FSO f4 -> i2
+  // and i2 -> f4, Quantize and AsType between f4 and f8
+  if (KIND == K_FSO_ENC && vec && db == MC_F4 && p.t1 == MC_F4 && p.t2 == MC_F4 && ab == MC_I2) {
+    launch_map_bo<KIND, MC_F4, MC_F4, MC_F4, MC_I2>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_FSO_DEC && vec && db == MC_I2 && p.t1 == MC_F8 && p.t2 == MC_F8 && ab == MC_F4) {
+    launch_map_bo<KIND, MC_I2, MC_F8, MC_F8, MC_F4>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_QUANTIZE && vec && db == MC_F4 && ab == MC_F4) {
+    launch_map_bo<KIND, MC_F4, MC_F4, MC_F4, MC_F4>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_CAST && vec && db == MC_F4 && ab == MC_F8) {  // AsType / Quantize decode
+    launch_map_bo<KIND, MC_F4, MC_F4, MC_F4, MC_F8, 2>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_CAST && vec && db == MC_F8 && ab == MC_F4) {
+    launch_map_bo<KIND, MC_F8, MC_F8, MC_F8, MC_F4, 2>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_CAST && vec && db == MC_F4 && ab == MC_F4) {  // byte order only
+    launch_map_bo<KIND, MC_F4, MC_F4, MC_F4, MC_F4>(sd, sa, grid, s, d, n, p, st);
+  } else if (KIND == K_QUANTIZE && vec && db == MC_F8 && ab == MC_F4) {
+    launch_map_bo<KIND, MC_F8, MC_F8, MC_F8, MC_F4, 2>(sd, sa, grid, s, d, n, p, st);
   } else if (vec && (mc_itemsize(p.d) == 8 || mc_itemsize(p.a) == 8)) {
     k_map<KIND, -1, -1, -1, -1, true, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, n, p);
   } else if (vec) {
@@ -404,6 +431,17 @@ static McNum num_scalar(int dt, double f, int64_t i) {
   r.f = mc_is_float(dt) ? f : 0.0;
   r.i = mc_is_float(dt) ? 0 : i;
   return r;
+}
+
+template <int ES>
+static void launch_delta_same(int sw, dim3 g, const uint8_t *s, uint8_t *d, size_t nbytes, size_t ss, size_t ds,
+                              hipStream_t st) {
+  switch (sw) {
+    case 0: k_delta_enc_same<ES, 0><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 1: k_delta_enc_same<ES, 1><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 2: k_delta_enc_same<ES, 2><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    default: k_delta_enc_same<ES, 3><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+  }
 }
 
 }  // namespace
@@ -496,15 +534,21 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
     const uint8_t *sc = s + c0 * src_stride;
     uint8_t *dc = d + c0 * dst_stride;
     // same-width integers: wrapping differences have the same bits whatever
-    // the signedness, so every such pair runs the signed instantiation
-    const int same = (dtype == astype && dtype != MC_B1 && !mc_is_float(dtype)) ? ss : 0;
+    // the signedness, so every such pair runs the signed instantiation; the
+    // constant-dtype k_delta_enc paths below are little-endian only (sw == 0)
+    const int db = mc_dt_base(dtype), ab = mc_dt_base(astype);
+    const int sw = (mc_dt_swapped(dtype) ? 1 : 0) | (mc_dt_swapped(astype) ? 2 : 0);
+    const int same = (db == ab && db != MC_B1 && !mc_is_float(db)) ? ss : 0;
     if (same && al16 && delta_enc_vec_enabled()) {
       const size_t per = (size_t)DE_V * 16 * MC_BLOCK;
       const dim3 g2((unsigned)((n * ss + per - 1) / per), grid.y);
       if (same == 1) k_delta_enc_same<1><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n, src_stride, dst_stride);
-      else if (same == 2) k_delta_enc_same<2><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 2, src_stride, dst_stride);
-      else if (same == 4) k_delta_enc_same<4><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 4, src_stride, dst_stride);
-      else k_delta_enc_same<8><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n * 8, src_stride, dst_stride);
+      else if (same == 2) launch_delta_same<2>(sw, g2, sc, dc, n * 2, src_stride, dst_stride, st);
+      else if (same == 4) launch_delta_same<4>(sw, g2, sc, dc, n * 4, src_stride, dst_stride, st);
+      else launch_delta_same<8>(sw, g2, sc, dc, n * 8, src_stride, dst_stride, st);
+    } else if (sw) {
+      if (vec) k_delta_enc<-1, -1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
+      else k_delta_enc<-1, -1, false><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, dtype, astype, src_stride, dst_stride);
     } else if (vec && same == 1)
       k_delta_enc<MC_I1, MC_I1, true><<<grid, MC_BLOCK, 0, st>>>(sc, dc, n, MC_I1, MC_I1, src_stride, dst_stride);
     else if (vec && same == 2)

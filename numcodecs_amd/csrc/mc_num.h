@@ -28,7 +28,7 @@ MC_HD McNum mc_num_i(int64_t i) { McNum r; r.f = 0.0; r.i = i; return r; }
 
 // wrap a 64-bit integer to dtype width (sign- or zero-extend back to 64 bits)
 MC_DEV int64_t mc_wrap(int64_t v, int dt) {
-  switch (dt) {
+  switch (mc_dt_base(dt)) {
     case MC_B1: return v != 0;
     case MC_I1: return (int64_t)(int8_t)v;
     case MC_I2: return (int64_t)(int16_t)v;
@@ -40,9 +40,11 @@ MC_DEV int64_t mc_wrap(int64_t v, int dt) {
   }
 }
 
-// raw little-endian bits (low itemsize bytes) -> value
+// raw bits (low itemsize bytes, as loaded little-endian) -> value; a
+// big-endian dtype's bytes are reversed first
 MC_DEV McNum mc_num_from_bits(uint64_t b, int dt) {
-  switch (dt) {
+  b = mc_to_storage(b, dt);
+  switch (mc_dt_base(dt)) {
     case MC_F2: return mc_num_f((double)mc_half_to_float((uint16_t)b));
     case MC_F4: return mc_num_f((double)mc_bits_f32((uint32_t)b));
     case MC_F8: return mc_num_f(mc_bits_f64(b));
@@ -51,18 +53,22 @@ MC_DEV McNum mc_num_from_bits(uint64_t b, int dt) {
   }
 }
 
-// value (already in dt) -> raw bits
+// value (already in dt) -> raw bits as stored (big-endian dtypes reversed)
 MC_DEV uint64_t mc_num_to_bits(McNum v, int dt) {
-  switch (dt) {
-    case MC_F2: return mc_float_to_half((float)v.f);  // exact: v.f holds a half value
-    case MC_F4: return mc_f32_bits((float)v.f);
-    case MC_F8: return mc_f64_bits(v.f);
-    default: return (uint64_t)v.i;
+  uint64_t b;
+  switch (mc_dt_base(dt)) {
+    case MC_F2: b = mc_float_to_half((float)v.f); break;  // exact: v.f holds a half value
+    case MC_F4: b = mc_f32_bits((float)v.f); break;
+    case MC_F8: b = mc_f64_bits(v.f); break;
+    default: b = (uint64_t)v.i; break;
   }
+  return mc_to_storage(b, dt);
 }
 
-// numpy astype(from -> to)
+// numpy astype(from -> to) (byte order is storage only: ignored here)
 MC_DEV McNum mc_num_cast(McNum v, int from, int to) {
+  from = mc_dt_base(from);
+  to = mc_dt_base(to);
   if (from == to) return v;
   const bool ff = mc_is_float(from), tf = mc_is_float(to);
   if (to == MC_B1) return mc_num_i(ff ? (v.f != 0.0) : (v.i != 0));
@@ -112,6 +118,7 @@ enum McOp { MC_OP_ADD, MC_OP_SUB, MC_OP_MUL, MC_OP_DIV };
 
 // a <op> b with both operands already in dtype dt
 MC_DEV McNum mc_num_binop(McNum a, McNum b, int op, int dt) {
+  dt = mc_dt_base(dt);
   if (dt == MC_F8) {
     double r;
     switch (op) {
@@ -153,6 +160,7 @@ MC_DEV McNum mc_num_binop(McNum a, McNum b, int op, int dt) {
 
 // np.around(x) == np.rint for floats (round half to even); identity for ints
 MC_DEV McNum mc_num_rint(McNum v, int dt) {
+  dt = mc_dt_base(dt);
   if (dt == MC_F8) return mc_num_f(__builtin_rint(v.f));
   if (dt == MC_F4) return mc_num_f((double)__builtin_rintf((float)v.f));
   if (dt == MC_F2) {

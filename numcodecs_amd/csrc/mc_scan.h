@@ -187,3 +187,110 @@ template <bool OR_OP>
 static inline void mc_launch_scan_sums_mw(const uint64_t *in, uint64_t *out, size_t n, hipStream_t st) {
   k_scan_sums_mw<OR_OP><<<(unsigned)((n + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(in, out, n);
 }
+
+// ---------------------------------------------------------------------------
+// Float Delta decode pieces shared by the serial chain (mc_scan.hip) and the
+// speculative path (mc_fspec.h, mc_fspec_f2/f4/f8.hip).
+// ---------------------------------------------------------------------------
+template <int D> struct SerAcc { using T = float; };
+template <> struct SerAcc<MC_F8> { using T = double; };
+
+template <int D>
+MC_DEV typename SerAcc<D>::T ser_add(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
+  if constexpr (D == MC_F2) {
+    // numpy's half loop: float32 add, then npy_float_to_half.  The hardware
+    // RNE conversion (denormals kept) gives the same half for every non-NaN
+    // sum; NaN sums take numpy's payload-preserving routine.
+    const float r = a + b;
+    if (__builtin_isnan(r)) return mc_half_to_float(mc_float_to_half(r));
+    return (float)(_Float16)r;
+  } else {
+    return a + b;
+  }
+}
+
+// G chain values as 16-B LDS accesses (p 16-B aligned)
+template <typename T, int SER_G>
+MC_DEV void ser_ld(const T *p, T (&r)[SER_G]) {
+  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int W = 16 / sizeof(T);
+#pragma unroll
+  for (int v = 0; v < SER_G / W; ++v) {
+    const vec x = reinterpret_cast<const vec *>(p)[v];
+#pragma unroll
+    for (int e = 0; e < W; ++e) r[v * W + e] = x[e];
+  }
+}
+template <typename T, int SER_G>
+MC_DEV void ser_st(T *p, const T (&r)[SER_G]) {
+  typedef T vec __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int W = 16 / sizeof(T);
+#pragma unroll
+  for (int v = 0; v < SER_G / W; ++v) {
+    vec x;
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = r[v * W + e];
+    reinterpret_cast<vec *>(p)[v] = x;
+  }
+}
+
+// numpy's loop dtype of cumsum(enc: a, out=dec: d) for a float d:
+// np.promote_types(a, d) (pinned against numpy for every pair by
+// tests/test_gpu_delta_spec2.py): the wider float; an integer promotes to the
+// smallest float that holds it (1-byte -> f2, 2-byte -> f4, wider -> f8)
+static inline int mc_float_loop_dtype(int a, int d) {
+  auto rank = [](int t) { return t == MC_F8 ? 3 : t == MC_F4 ? 2 : t == MC_F2 ? 1 : 0; };
+  a = mc_dt_base(a);
+  d = mc_dt_base(d);
+  int fa;
+  if (mc_is_float(a)) fa = a;
+  else if (a == MC_B1 || mc_itemsize(a) == 1) fa = MC_F2;
+  else if (mc_itemsize(a) == 2) fa = MC_F4;
+  else fa = MC_F8;
+  return rank(fa) > rank(d) ? fa : d;
+}
+
+// the speculative path's tile: FS_Q 16-B vectors per thread of W elements
+constexpr int FS_Q = 4;
+MC_HD constexpr int fs_w_of(int d) { return d == MC_F8 ? 2 : (d == MC_F4 ? 4 : 8); }
+MC_HD constexpr size_t fs_tile_of(int d) { return (size_t)fs_w_of(d) * FS_Q * MC_BLOCK; }
+
+static inline size_t fspec_ntiles(size_t n, int dt) {
+  const size_t te = fs_tile_of(mc_dt_base(dt));
+  return (n + te - 1) / te;
+}
+
+// the speculative decode serves any float dtype D with any numeric astype
+// except bool whose loop dtype is D (casts as numpy's cumsum(enc, out=dec)
+// does); a wider loop dtype (f8 astype into f4, ...) runs the serial chain
+static inline bool fspec_types_ok(int astype, int dtype) {
+  // the fix-up restarts from dtype values, so the loop dtype must be dtype
+  return mc_is_float(dtype) && mc_valid_dtype(astype) && astype != MC_B1 &&
+         mc_float_loop_dtype(astype, dtype) == mc_dt_base(dtype);
+}
+
+// tile totals, tile prefixes, per-tile first failures, the first failure
+// (the last word, read by the tests)
+static inline size_t fspec_ws_bytes(size_t n, int dt) { return (3 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
+
+// speculative float Delta decode of one chunk (workspace fspec_ws_bytes) /
+// of `g` rows (fail: one word per row), output dtype f2 / f4 / f8, any
+// astype whose loop dtype is the output dtype (mc_fspec_f*.hip); the _be_
+// twins take a big-endian astype `a` and/or output (swo)
+#define MC_FSPEC_DECL(T)                                                                                          \
+  void mc_fspec_launch_##T(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st);            \
+  void mc_fspec_rows_launch_##T(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,           \
+                                uint64_t *fail, unsigned g, hipStream_t st);                                   \
+  void mc_fspec_launch_be_##T(const uint8_t *s, uint8_t *d, size_t n, int a, bool swo, void *ws, hipStream_t st); \
+  void mc_fspec_rows_launch_be_##T(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,        \
+                                   bool swo, uint64_t *fail, unsigned g, hipStream_t st);
+MC_FSPEC_DECL(f2)
+MC_FSPEC_DECL(f4)
+MC_FSPEC_DECL(f8)
+#undef MC_FSPEC_DECL
+
+// numpy's serial float chain over `rows` chunks of n elements (astype a, may
+// be big-endian; float dtype dt, may be big-endian); variant 0 = default
+// schedule (mc_scan_serial.hip)
+void mc_launch_serial_any(const uint8_t *s, size_t ss, uint8_t *d, size_t dss, size_t n, size_t rows, int a, int dt,
+                          hipStream_t st, int variant = 0);

@@ -636,25 +636,42 @@ static constexpr int V_GROUP_SHIFT = 5;
 static constexpr int V_GROUP_MASK = 3 << V_GROUP_SHIFT;
 // variant | V_PIPE: software-pipelined persistent loop (register layout only)
 static constexpr int V_PIPE = 256;
+// variant | V_BIG8 selects 8x larger tiles (register and lane-pair layouts)
+static constexpr int V_BIG8 = 512;
+static constexpr int V_TILE_MASK = V_BIG | V_BIG4 | V_BIG8;
 
-// Measured defaults (tools/probe_enc.py on MI355X, interleaved rounds; the
-// sweep is summarised in DESIGN.md).  Large buffers: one big tile per
-// workgroup and a grid covering every tile (a looping workgroup waits for its
-// previous tile's stores before it can use the next tile's loads, because
-// vmcnt retires loads and stores in issue order).  Small buffers: 4096-element
-// tiles so that there are enough workgroups.
-static int default_variant(size_t es, bool enc, size_t total_bytes, unsigned *grid_cap) {
+// Measured defaults (tools/probe_enc.py, tools/probe_shuffle_tiles.py on
+// MI355X, interleaved rounds; the sweeps are summarised in DESIGN.md).  Large
+// buffers: one big tile per workgroup and a grid covering every tile (a
+// looping workgroup waits for its previous tile's stores before it can use
+// the next tile's loads, because vmcnt retires loads and stores in issue
+// order).  Small buffers: 4096-element tiles so that there are enough
+// workgroups.  A tile multiplier is only used where it leaves (almost) no
+// elements to the byte-granular tail kernel: `count` a multiple of the
+// tile, or at least 64 tiles per chunk.
+static int tile_flag(size_t count, size_t base_elems, int want) {
+  for (int flag = want; flag; flag = flag == V_BIG8 ? V_BIG4 : flag == V_BIG4 ? V_BIG : 0) {
+    const size_t m = flag == V_BIG8 ? 8 : flag == V_BIG4 ? 4 : 2;
+    if (count % (base_elems * m) == 0 || count >= 64 * base_elems * m) return flag;
+  }
+  return 0;
+}
+
+static int default_variant(size_t es, bool enc, size_t total_bytes, size_t count, unsigned *grid_cap) {
   *grid_cap = 0x7fffffffu;
   if (total_bytes < ((size_t)64 << 20)) return V_REG;
   switch (es) {
-    case 2: return V_REG | V_BIG4;                       // 6.34 / 6.22 TB/s
-    // decode: lane pairs, 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
-    // profiles/r01/shuffle4_pair_ab.log); encode: the pair stores are slower
-    case 4: return enc ? (V_REG | V_BIG4) : (V_PAIR | V_BIG);
+    case 2: return V_REG | tile_flag(count, 4096, V_BIG4);  // 6.34 / 6.22 TB/s
+    // encode: 32768-element tiles (128 KiB per workgroup, 32 16-B loads in
+    // flight per thread): 87.5 against 93.0 us for 64 KiB tiles, 256 MiB
+    // (round 4, profiles/r04/probe_shuffle_tiles.json); decode: lane pairs,
+    // 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
+    // profiles/r01/shuffle4_pair_ab.log; larger pair tiles measured slower)
+    case 4: return enc ? (V_REG | tile_flag(count, 4096, V_BIG8)) : (V_PAIR | tile_flag(count, 4096, V_BIG));
     case 8:  // lane pairs keep the 8-B element side lane-contiguous
-      return enc ? V_PAIR : (V_PAIR | V_BIG);            // 5.89 / 6.11 TB/s
+      return enc ? V_PAIR : (V_PAIR | tile_flag(count, 2048, V_BIG));  // 5.89 / 6.11 TB/s
     default:
-      if (enc) return V_REG | V_BIG;
+      if (enc) return V_REG | tile_flag(count, 2048, V_BIG);
       *grid_cap = MC_MAX_GRID;
       return V_BOTH_LDS;
   }
@@ -672,7 +689,8 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
       return;
     }
     if ((layout & 7) == V_PAIR) {
-      if (layout & V_BIG4) k_shuffle4_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      if (layout & V_BIG8) k_shuffle4_enc_pair<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG4) k_shuffle4_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else if (layout & V_BIG) k_shuffle4_enc_pair<BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else k_shuffle4_enc_pair<BR, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       return;
@@ -686,7 +704,8 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
       return;
     }
     if ((layout & 7) == V_PAIR) {
-      if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      if (layout & V_BIG8) k_shuffle8_enc_pair<BR, NT, 32><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else if (layout & V_BIG) k_shuffle8_enc_pair<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else k_shuffle8_enc_pair<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       return;
@@ -698,6 +717,8 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     k_shuffle_enc_pipe<ES, BR, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
   else if (layout == (V_REG | V_PIPE))
     k_shuffle_enc_pipe<ES, BR, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+  else if (layout == (V_REG | V_BIG8))
+    k_shuffle_enc<ES, BR, false, false, NT, (ES <= 8 ? 8 : 4)><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
   else if (layout == (V_REG | V_BIG4))
     k_shuffle_enc<ES, BR, false, false, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
   else if (layout == (V_REG | V_BIG))
@@ -714,10 +735,11 @@ template <int ES, bool BR>
 static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                             size_t ntiles, unsigned grid, const McBitRound &br,
                             hipStream_t st) {
-  const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
+  const int layout = variant & (7 | V_TILE_MASK | V_PIPE);
   if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
-  if ((layout & 7) == V_WIDE && ((ES != 4 && ES != 8) || (layout & V_PIPE))) return MC_EINVAL;
+  if ((layout & 7) == V_WIDE && ((ES != 4 && ES != 8) || (layout & (V_PIPE | V_BIG8)))) return MC_EINVAL;
+  if ((layout & V_BIG8) && (layout & V_PIPE)) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
   else launch_enc_nt<ES, BR, true>(layout, s, d, m, ntiles, grid, br, st);
   return mc_last_launch();
@@ -729,7 +751,8 @@ static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
   using G = Geom<ES>;
   if constexpr (ES == 4) {
     if ((layout & 7) == V_PAIR) {
-      if (layout & V_BIG4) k_shuffle4_dec_pair<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      if (layout & V_BIG8) k_shuffle4_dec_pair<NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else if (layout & V_BIG4) k_shuffle4_dec_pair<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       else if (layout & V_BIG) k_shuffle4_dec_pair<NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       else k_shuffle4_dec_pair<NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       return;
@@ -743,7 +766,8 @@ static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
       return;
     }
     if ((layout & 7) == V_PAIR) {
-      if (layout & V_BIG4) k_shuffle8_dec_pair<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      if (layout & V_BIG8) k_shuffle8_dec_pair<NT, 32><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+      else if (layout & V_BIG4) k_shuffle8_dec_pair<NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       else if (layout & V_BIG) k_shuffle8_dec_pair<NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       else k_shuffle8_dec_pair<NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
       return;
@@ -755,6 +779,8 @@ static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     k_shuffle_dec_pipe<ES, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
   else if (layout == (V_REG | V_PIPE))
     k_shuffle_dec_pipe<ES, NT, 1><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
+  else if (layout == (V_REG | V_BIG8))
+    k_shuffle_dec<ES, false, false, NT, (ES <= 8 ? 8 : 4)><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
   else if (layout == (V_REG | V_BIG4))
     k_shuffle_dec<ES, false, false, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles);
   else if (layout == (V_REG | V_BIG))
@@ -770,23 +796,25 @@ static void launch_dec_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
 template <int ES>
 static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const ChunkMap &m,
                             size_t ntiles, unsigned grid, hipStream_t st) {
-  const int layout = variant & (7 | V_BIG | V_BIG4 | V_PIPE);
+  const int layout = variant & (7 | V_TILE_MASK | V_PIPE);
   if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
-  if ((layout & 7) == V_WIDE && (ES != 8 || (layout & V_PIPE))) return MC_EINVAL;
+  if ((layout & 7) == V_WIDE && (ES != 8 || (layout & (V_PIPE | V_BIG8)))) return MC_EINVAL;
+  if ((layout & V_BIG8) && (layout & V_PIPE)) return MC_EINVAL;
   if (variant & V_NO_NT) launch_dec_nt<ES, false>(layout, s, d, m, ntiles, grid, st);
   else launch_dec_nt<ES, true>(layout, s, d, m, ntiles, grid, st);
   return mc_last_launch();
 }
 
 static size_t tile_elems(size_t es, int variant) {
+  const size_t mul = (variant & V_BIG8) ? 8 : (variant & V_BIG4) ? 4 : (variant & V_BIG) ? 2 : 1;
   if (((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) && es == 4)  // Geom<4, QMUL> tiles
-    return (variant & V_BIG4) ? 16384 : (variant & V_BIG) ? 8192 : 4096;
+    return 4096 * mul;
   if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE)  // 256 lanes x NV 16-B units of 8-B elements
-    return (variant & V_BIG4) ? 8192 : (variant & V_BIG) ? 4096 : 2048;
+    return 2048 * mul;
   const size_t te = es >= 16 ? 2048 : 4096;
   if ((variant & 7) != V_REG) return te;
-  return (variant & V_BIG4) ? 4 * te : (variant & V_BIG) ? 2 * te : te;
+  return te * mul;
 }
 
 }  // namespace
@@ -816,7 +844,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
 
   unsigned default_cap = MC_MAX_GRID;
   if (variant == V_DEFAULT) {
-    variant = default_variant(es, enc, chunk_bytes * nchunks, &default_cap);
+    variant = default_variant(es, enc, chunk_bytes * nchunks, m.count, &default_cap);
     if (max_blocks <= 0) max_blocks = (int)default_cap;
   }
   const bool fast_es = es == 2 || es == 4 || es == 8 || es == 16;
@@ -826,7 +854,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   // the 16-B plane-side accesses need 16-B aligned plane bases
   if ((variant & 7) != V_GENERIC && (variant & 7) != V_REG && (variant & 7) != V_PAIR &&
       m.count % 16 != 0)
-    variant = V_REG | (variant & (V_NO_NT | V_BIG | V_BIG4 | V_GROUP_MASK | V_PIPE));
+    variant = V_REG | (variant & (V_NO_NT | V_TILE_MASK | V_GROUP_MASK | V_PIPE));
 
   size_t e_done = 0;
   McBitRound nobr{};
@@ -835,9 +863,11 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
     if ((variant & 7) == V_PAIR && es != 8 && es != 4) variant = V_REG | (variant & V_NO_NT);
     if ((variant & 7) == V_WIDE && !(es == 8 || (es == 4 && enc))) variant = V_REG | (variant & V_NO_NT);
     if ((variant & 7) != V_REG && (variant & 7) != V_PAIR && (variant & 7) != V_WIDE)
-      variant &= ~(V_BIG | V_BIG4 | V_PIPE);
+      variant &= ~(V_TILE_MASK | V_PIPE);
     if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) variant &= ~V_PIPE;
-    if (variant & V_PIPE) variant &= ~V_GROUP_MASK;
+    if ((variant & 7) == V_WIDE || es == 16) variant &= ~V_BIG8;
+    if (variant & V_PIPE) variant &= ~(V_GROUP_MASK | V_BIG8);
+    if (variant & V_BIG8) variant &= ~(V_BIG | V_BIG4);
     if (variant & V_BIG4) variant &= ~V_BIG;
     m.group = 1u << ((variant & V_GROUP_MASK) >> V_GROUP_SHIFT);
     const size_t te = tile_elems(es, variant);

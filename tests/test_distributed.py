@@ -71,34 +71,40 @@ def test_chunk_range_and_aggregate():
     assert aggregate_gibps(8 * (1 << 30), 2.0) == 4.0
 
 
-def test_bench_self_launches_ranks_dry_run():
-    """`bench.py --gpus 2` with no launcher starts two rank processes itself
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_self_launches_ranks_dry_run(world):
+    """`bench.py --gpus N` with no launcher starts N rank processes itself
     (torch.distributed env set per child, gloo here: --dry-run touches no
     GPU); their contiguous ranges cover all 8192 C5 chunks exactly once and
-    every rank round-trips a sample of its chunks through the oracle."""
+    every rank round-trips a sample of its chunks through the oracle.  N = 8
+    rehearses the driver's 8-GPU node: 8 distinct rank processes."""
     import json
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints the one line
     d = json.loads(lines[0])
-    assert d["n_ranks"] == 2 and d["chunks"] == 8192 and d["covered_all"]
-    assert [x["range"] for x in d["ranks"]] == [[0, 4096], [4096, 8192]]
-    assert len({x["pid"] for x in d["ranks"]}) == 2 and os.getpid() not in {x["pid"] for x in d["ranks"]}
-    assert all(x["ok"] for x in d["ranks"]) and d["max_over_ranks"] == 1.0
+    per = 8192 // world
+    assert d["n_ranks"] == world and d["chunks"] == 8192 and d["covered_all"]
+    assert [x["range"] for x in d["ranks"]] == [[k * per, (k + 1) * per] for k in range(world)]
+    assert len({x["pid"] for x in d["ranks"]}) == world and os.getpid() not in {x["pid"] for x in d["ranks"]}
+    assert all(x["ok"] for x in d["ranks"]) and d["max_over_ranks"] == float(world - 1)
     # the N-GPU record the GPU line carries, labelled as a rehearsal
-    assert [x["rank"] for x in d["ranks"]] == [0, 1]
+    assert [x["rank"] for x in d["ranks"]] == list(range(world))
     assert all(x["device"] == "cpu" and x["elapsed_s"] > 0 for x in d["ranks"])
     assert d["rehearsal"] is True and d["physical_gpus"] == 0
     assert d["per_gpu_GiBps"] is None and d["frac_of_n_peak"] is None
     assert d["aggregate_GiBps"] > 0
-    assert abs(d["per_rank_GiBps"] * 2 - d["aggregate_GiBps"]) <= 1e-5 * d["aggregate_GiBps"]
+    assert abs(d["per_rank_GiBps"] * world - d["aggregate_GiBps"]) <= 1e-5 * d["aggregate_GiBps"]
+    # per-rank GPU-event times exist in the record (none on a CPU rehearsal)
+    assert all("gpu_event_s" in x for x in d["ranks"])
+    assert d["event_aggregate_GiBps"] is None and "host_minus_event_s" in d
 
 
 def test_scaling_fields_physical_gpus():
@@ -113,6 +119,11 @@ def test_scaling_fields_physical_gpus():
     assert f["physical_gpus"] == 4 and f["rehearsal"] is False
     assert f["aggregate_GiBps"] == 16.0 and f["per_gpu_GiBps"] == 4.0 and f["per_rank_GiBps"] == 4.0
     assert f["frac_of_n_peak"] == 1.0  # 4 x 8e12 B in 1 s over 4 x 8 TB/s
+    assert f["event_aggregate_GiBps"] is None  # no per-rank event times given
+    timed = [dict(mk(r, f"0000:{r:02x}:00"), gpu_event_s=0.5 + 0.1 * r) for r in range(4)]
+    f2 = bench.scaling_fields(timed, 8e12, 4 * GiB, 1.0, on_gpu=True)
+    assert f2["event_t_max_s"] == 0.8 and f2["event_aggregate_GiBps"] == 20.0
+    assert abs(f2["host_minus_event_s"] - 0.2) < 1e-9
     shared = [mk(r, "0000:03:00") for r in range(2)]
     g = bench.scaling_fields(shared, 8e12, GiB, 2.0, on_gpu=True)
     assert g["physical_gpus"] == 1 and g["rehearsal"] is True

@@ -39,8 +39,9 @@ def test_shuffle_every_variant(device, es):
     without a tail, through the tuning entry point."""
     st = torch.cuda.current_stream().cuda_stream
     lib = lab_lib()
-    variants = [1, 2, 3, 4, 9, 10, 11, 17, 129, 33, 65, 257, 273, 385, 5, 21, 133, 6, 22, 134]
-    for count in (4096 * 16 + 64, 16384 * 8, 4096 * 3 + 4):
+    variants = [1, 2, 3, 4, 9, 10, 11, 17, 129, 33, 65, 257, 273, 385, 5, 21, 133, 6, 22, 134,
+                513, 517, 518, 521, 769]  # | 512: 8x tiles (518 / 769 fall back to valid layouts)
+    for count in (4096 * 16 + 64, 16384 * 8, 4096 * 3 + 4, 32768 * 4 + 8):
         n = es * count
         x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=device)
         ref = oracle.shuffle(x.cpu().numpy(), es)
@@ -72,7 +73,7 @@ def test_shuffle_misaligned_views(device):
 @pytest.mark.parametrize("dt,kmax", [("<f2", 10), ("<f4", 23), ("<f8", 52)])
 def test_bitround_shuffle_fused(device, dt, kmax):
     es = np.dtype(dt).itemsize
-    for count in (4096 * 8, 4096 * 8 + 4, 1000, 65536 * 3):
+    for count in (4096 * 8, 4096 * 8 + 4, 1000, 65536 * 3, (64 << 20) // es + 32768 * 2 + 4):
         bits = RNG.integers(0, 2**63, count, dtype=np.uint64)
         x = bits.astype({2: np.uint16, 4: np.uint32, 8: np.uint64}[es]).view(dt)
         xd = torch.from_numpy(x.copy()).to(device)

@@ -23,6 +23,8 @@
 //           transpose (not a shuffle; a ceiling for the layout)
 //   kind 8  register staging, Q = 32 (two tiles' loads in flight per thread)
 //   kind 9  as 4 with default-policy LDS-DMA loads
+//   kind 10 as 8 with the quad-major store order
+//   kind 11 register staging, Q = 64 (four tiles' loads in flight)
 #include "mc_shuffle.h"
 
 namespace {
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_quadlane(const uint8_t *_
 
 extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, int kind, mc_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
-  const int Q = (kind == 4 || kind == 9) ? 8 : kind == 8 ? 32 : 16;
+  const int Q = (kind == 4 || kind == 9) ? 8 : (kind == 8 || kind == 10) ? 32 : kind == 11 ? 64 : 16;
   const size_t tb = (size_t)Q * 4 * MC_BLOCK * 4;  // tile bytes
   if (!src || !dst || nbytes == 0 || nbytes % tb || (uintptr_t)src % 16 || (uintptr_t)dst % 16) return MC_EINVAL;
   const size_t count = nbytes / 4, ntiles = nbytes / tb;
@@ -158,6 +160,8 @@ extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, in
     case 6: k_lab_enc4_quadlane<16><<<g, MC_BLOCK, 0, st>>>(s, d, count); break;
     case 7: k_lab_enc4_reg<16, 0, false, false><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 8: k_lab_enc4_reg<32, 0, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 10: k_lab_enc4_reg<32, 1, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 11: k_lab_enc4_reg<64, 0, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();

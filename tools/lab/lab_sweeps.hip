@@ -42,11 +42,25 @@ int mc_lab_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype,
 // bits 0-2 layout (0 default, 1 register/dword stores, 2 LDS-staged 16-B
 // stores, 3 LDS both sides, 4 generic byte kernel, 5 lane pairs), | 8
 // temporal accesses, | 16 / | 128 2x / 4x tiles, bits 5-6 tile group,
-// | 256 software-pipelined persistent loop; max_blocks 0 = default grid.
+// | 256 software-pipelined persistent loop, | 512 8x tiles; max_blocks 0 =
+// default grid.
 int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize, int encode,
                            int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x1FF) != 0) return MC_EINVAL;
+  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
   return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
+                         (hipStream_t)stream);
+}
+
+// BitRound fused into the Shuffle encode (mc_bitround_shuffle) with an
+// explicit layout, as mc_lab_shuffle_variant.
+int mc_lab_bitround_shuffle_variant(const void *src, void *dst, size_t n, int itemsize, int keepbits,
+                                    int variant, int max_blocks, mc_stream_t stream) {
+  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  if (!(itemsize == 2 || itemsize == 4 || itemsize == 8)) return MC_EINVAL;
+  const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
+  if (keepbits < 0 || keepbits >= mbits) return MC_EINVAL;
+  const McBitRound br = mc_make_bitround(itemsize, keepbits);
+  return mc_shuffle_impl(src, 0, dst, 0, 1, n * (size_t)itemsize, (size_t)itemsize, true, variant, max_blocks, &br,
                          (hipStream_t)stream);
 }
 
