@@ -17,8 +17,10 @@
 //     (es = 2) accesses per lane; the plane side either directly with one
 //     dword per lane per plane (256 contiguous bytes per wave instruction) or
 //     staged through LDS so that it too moves 16 B per lane (1 KiB per wave
-//     instruction).  Which combination is fastest is measured (bench.py
-//     --sweep) and the winner per (es, direction) is the default.
+//     instruction).  Which combination is fastest is measured
+//     (tools/probe_enc.py, tools/probe_shuffle_tiles.py: interleaved
+//     sweeps through the lab library) and the winner per (es, direction)
+//     is the default.
 //   * Sizes that are not a whole number of tiles finish with a generic
 //     byte-granular kernel over the tail elements; unaligned buffers or
 //     count % 4 != 0 run entirely on the generic kernel.

@@ -1,3 +1,3 @@
-# C4 fused enc/dec timing (bench.py --extra), two runs
+# C4 fused enc/dec timing (bench.py's cfg_C4 entry of the default run), two runs
 set -e
-for r in 1 2; do timeout -k 10 300 python bench.py --extra --no-cpu --steps 10 2>/dev/null | grep '^{' | python3 -c 'import json,sys; d=json.loads(sys.stdin.read())["extra"]; print({k: v for k, v in d.items() if "C4" in k})'; done
+for r in 1 2; do timeout -k 10 400 python bench.py --no-cpu --steps 10 2>/dev/null | grep '^{' | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["cfg_C4"])'; done
