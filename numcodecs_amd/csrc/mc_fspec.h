@@ -52,20 +52,28 @@ namespace {
 // by element and casts.  The double-precision scan only proposes candidates;
 // the per-element check against that recurrence decides, so the candidate
 // rounding (double -> D) need not match numpy's.
-template <int D> struct FsStore { using S = float; using V = float; };
-template <> struct FsStore<MC_F8> { using S = double; using V = double; };
-template <> struct FsStore<MC_F2> { using S = _Float16; using V = float; };
+// P: the precision of the candidate scan (double; float for f2, whose
+// 11-bit values sum exactly in float32 over a tile of smooth data and whose
+// double scan made the f2 instances VALU-bound -- any precision only
+// proposes, the per-element check decides)
+template <int D> struct FsStore { using S = float; using V = float; using P = double; };
+template <> struct FsStore<MC_F8> { using S = double; using V = double; using P = double; };
+template <> struct FsStore<MC_F2> { using S = _Float16; using V = float; using P = float; };
 
 template <int A_, int D>
 struct FsT {
   using S = typename FsStore<D>::S;  // stored element
   using V = typename FsStore<D>::V;  // arithmetic value (numpy's loop type)
+  using P = typename FsStore<D>::P;  // candidate scan precision
   static constexpr int W = 16 / (int)sizeof(S);
   typedef S svec __attribute__((ext_vector_type(W)));
   MC_DEV static V from_bits(uint64_t bits, int a) {  // enc element -> its D value
     return (V)mc_num_cast(mc_num_from_bits(bits, a), a, D).f;
   }
-  MC_DEV static S round(double x) { return (S)x; }  // candidate (any rounding)
+  MC_DEV static S round(P x) { return (S)x; }  // candidate (any rounding)
+  // the last candidate of a tile from its (double) tile prefix and total, as
+  // the apply pass / walker computed it there (bitwise)
+  MC_DEV static S bound(double pre, double sum) { return round((P)pre + (P)sum); }
   MC_DEV static V val(S c) { return (V)c; }
   MC_DEV static S store(V r) { return (S)r; }  // exact: r holds a D value
   MC_DEV static V step(V pv, V x) { return ser_add<D>(pv, x); }
@@ -229,36 +237,57 @@ MC_DEV double mc_wave_scan_f64(double x) {
 // lane i <- lane i - 1 (lane 0 <- -0.0)
 MC_DEV double mc_wave_shr1_f64(double x) { return mc_dpp_f64<0x138, 0xF>(x); }
 
-template <typename V, int W>
-MC_DEV void fs_tile_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double (&lds)[FS_Q][MC_BLOCK / 64]) {
+// the same for one float per lane (6 DPP-sourced adds)
+template <int CTRL, int ROW_MASK>
+MC_DEV float mc_dpp_f32(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp((int)0x80000000u, __builtin_bit_cast(int, x), CTRL,
+                                                               ROW_MASK, 0xF, false));
+}
+MC_DEV float mc_wave_scan_f32(float x) {
+  x = x + mc_dpp_f32<0x111, 0xF>(x);
+  x = x + mc_dpp_f32<0x112, 0xF>(x);
+  x = x + mc_dpp_f32<0x114, 0xF>(x);
+  x = x + mc_dpp_f32<0x118, 0xF>(x);
+  x = x + mc_dpp_f32<0x142, 0xA>(x);
+  x = x + mc_dpp_f32<0x143, 0xC>(x);
+  return x;
+}
+MC_DEV float mc_wave_shr1_f32(float x) { return mc_dpp_f32<0x138, 0xF>(x); }
+MC_DEV double mc_wave_scan_p(double x) { return mc_wave_scan_f64(x); }
+MC_DEV float mc_wave_scan_p(float x) { return mc_wave_scan_f32(x); }
+MC_DEV double mc_wave_shr1_p(double x) { return mc_wave_shr1_f64(x); }
+MC_DEV float mc_wave_shr1_p(float x) { return mc_wave_shr1_f32(x); }
+
+template <typename V, int W, typename P>
+MC_DEV void fs_tile_scan(const V (&v)[FS_Q][W], P (&p)[FS_Q][W], P (&lds)[FS_Q][MC_BLOCK / 64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double incl[FS_Q];
+  P incl[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
-    p[q][0] = (double)v[q][0];
+    p[q][0] = (P)v[q][0];
 #pragma unroll
-    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (double)v[q][e];
+    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (P)v[q][e];
     incl[q] = p[q][W - 1];
   }
 #pragma unroll
-  for (int q = 0; q < FS_Q; ++q) incl[q] = mc_wave_scan_f64(incl[q]);
-  double ex[FS_Q];
+  for (int q = 0; q < FS_Q; ++q) incl[q] = mc_wave_scan_p(incl[q]);
+  P ex[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
     if (lane == 63) lds[q][wave] = incl[q];
-    ex[q] = mc_wave_shr1_f64(incl[q]);
+    ex[q] = mc_wave_shr1_p(incl[q]);
   }
   __syncthreads();
-  double base = 0.0;
+  P base = 0;
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
-    double w = 0.0, tot = 0.0;
+    P w = 0, tot = 0;
 #pragma unroll
     for (int j = 0; j < MC_BLOCK / 64; ++j) {
       if (j < wave) w = w + lds[q][j];
       tot = tot + lds[q][j];
     }
-    const double pre = base + (lane ? w + ex[q] : w);
+    const P pre = base + (lane ? w + ex[q] : w);
 #pragma unroll
     for (int e = 0; e < W; ++e) p[q][e] = pre + p[q][e];
     base = base + tot;
@@ -296,13 +325,14 @@ template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n, int a,
                                                           double *__restrict__ sums) {
   using Tr = FsT<A_, D>;
+  using P = typename Tr::P;
   constexpr int W = Tr::W;
-  __shared__ double lds[FS_Q][MC_BLOCK / 64];
+  __shared__ P lds[FS_Q][MC_BLOCK / 64];
   typename Tr::V v[FS_Q][W];
   fs_load<A_, D, SW>(src, n, (size_t)blockIdx.x * fs_tile<D>(), a, v);
-  double p[FS_Q][W];
-  fs_tile_scan<typename Tr::V, W>(v, p, lds);
-  if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = p[FS_Q - 1][W - 1];
+  P p[FS_Q][W];
+  fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
+  if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = (double)p[FS_Q - 1][W - 1];
 }
 
 template <int A_, int D, int SW = 0>
@@ -314,8 +344,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
                                                          uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
+  using P = typename Tr::P;
   constexpr int W = Tr::W;
-  __shared__ double lds[FS_Q][MC_BLOCK / 64];
+  __shared__ P lds[FS_Q][MC_BLOCK / 64];
   __shared__ S ldsc[FS_Q][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t tile = blockIdx.x;
@@ -325,9 +356,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   // over the tiles recorded here as verified once it is back in sync
   typename Tr::V v[FS_Q][W];
   fs_load<A_, D, SW>(src, n, t0, a, v);
-  double p[FS_Q][W];
-  fs_tile_scan<typename Tr::V, W>(v, p, lds);
-  const double Sp = pre_t[tile];  // the tile's prefix
+  P p[FS_Q][W];
+  fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
+  const P Sp = (P)pre_t[tile];  // the tile's prefix
   S c[FS_Q][W], up[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -339,7 +370,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   __syncthreads();
   // the tile's last candidate in the previous tile: the same double sum it
   // was rounded from there (sums[] is that tile's last prefix, bitwise)
-  const S pbound = tile ? Tr::round(pre_t[tile - 1] + sums[tile - 1]) : (S)0;
+  const S pbound = tile ? Tr::bound(pre_t[tile - 1], sums[tile - 1]) : (S)0;
   S p0[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -375,15 +406,16 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
                                                         uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
+  using P = typename Tr::P;
   constexpr int W = Tr::W;
-  __shared__ double lds[2][FS_Q][MC_BLOCK / 64];
+  __shared__ P lds[2][FS_Q][MC_BLOCK / 64];
   __shared__ S ldsc[2][FS_Q][MC_BLOCK / 64];
   __shared__ uint64_t ldsf[2][MC_BLOCK / 64];
-  __shared__ double ldsp[2];
+  __shared__ P ldsp[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   src += (size_t)blockIdx.x * src_stride;
   dst += (size_t)blockIdx.x * dst_stride;
-  double carry = 0.0;
+  P carry = 0;
   S prevc = (S)0;
   int par = 0;
   typename Tr::V nv[FS_Q][W];
@@ -395,8 +427,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
 #pragma unroll
       for (int e = 0; e < W; ++e) v[q][e] = nv[q][e];
     if (t0 + fs_tile<D>() < n) fs_load<A_, D, SW>(src, n, t0 + fs_tile<D>(), a, nv);  // next tile in flight
-    double p[FS_Q][W];
-    fs_tile_scan<typename Tr::V, W>(v, p, lds[par]);
+    P p[FS_Q][W];
+    fs_tile_scan<typename Tr::V, W, P>(v, p, lds[par]);
     S c[FS_Q][W], up[FS_Q];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q) {
@@ -633,25 +665,25 @@ MC_DEV void fsw_store(uint8_t *dst, size_t n, size_t t0, const typename FsT<A_, 
 // p[q][e] = the tile-relative inclusive double prefix of this thread's
 // elements in the walker layout (any fixed association: candidates only
 // propose, the per-element check decides)
-template <typename V, int W>
-MC_DEV void fsw_scan(const V (&v)[FS_Q][W], double (&p)[FS_Q][W], double *ldsq) {
+template <typename V, int W, typename P>
+MC_DEV void fsw_scan(const V (&v)[FS_Q][W], P (&p)[FS_Q][W], P *ldsq) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double base = 0.0;
+  P base = 0;
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
-    p[q][0] = (double)v[q][0];
+    p[q][0] = (P)v[q][0];
 #pragma unroll
-    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (double)v[q][e];
-    const double incl = mc_wave_scan_f64(p[q][W - 1]);
-    const double ex = mc_wave_shr1_f64(incl);
-    const double pre = base + (lane ? ex : 0.0);
+    for (int e = 1; e < W; ++e) p[q][e] = p[q][e - 1] + (P)v[q][e];
+    const P incl = mc_wave_scan_p(p[q][W - 1]);
+    const P ex = mc_wave_shr1_p(incl);
+    const P pre = base + (lane ? ex : (P)0);
 #pragma unroll
     for (int e = 0; e < W; ++e) p[q][e] = pre + p[q][e];
     base = base + fsw_readlane(incl, 63);
   }
   if (lane == 0) ldsq[wave] = base;  // the quarter's total
   __syncthreads();
-  double off = 0.0;
+  P off = 0;
 #pragma unroll
   for (int w = 0; w < FSW_NW; ++w)
     if (w < wave) off = off + ldsq[w];
@@ -800,16 +832,17 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
   using V = typename Tr::V;
+  using P = typename Tr::P;
   constexpr int W = Tr::W;
   constexpr int TE = (int)fs_tile<D>();
   constexpr int QE = fsw_qe<D>();
   constexpr int NOFAIL = 0x7fffffff;
   // per pass, each wave publishes its last candidate, its first element
   // (value, candidate, prefix) and its first failure inside the quarter
-  __shared__ double ldsq[FSW_NW];
+  __shared__ P ldsq[FSW_NW];
   __shared__ S lds_last[2][FSW_NW], lds_bc[2][FSW_NW], lds_fv[2][FSW_NW];
   __shared__ V lds_bv[2][FSW_NW];
-  __shared__ double lds_bp[2][FSW_NW], lds_fp[2][FSW_NW];
+  __shared__ P lds_bp[2][FSW_NW], lds_fp[2][FSW_NW];
   __shared__ int lds_fi[2][FSW_NW];
   __shared__ uint64_t ldsx[FSW_NW];
   __shared__ S ldsy;
@@ -828,7 +861,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     if (f >= n) return;        // everything verified: dst is final
     t = (size_t)(f / TE);
     has_in = t > 0;
-    if (has_in) yin = Tr::round(pre[t - 1] + sums[t - 1]);  // tile t-1 verified: its last candidate
+    if (has_in) yin = Tr::bound(pre[t - 1], sums[t - 1]);  // tile t-1 verified: its last candidate
   } else {
     // a row that k_fspec_rows left at its first failing tile (rowfail = its
     // start; n when the row verified): resume there from the last stored value
@@ -855,12 +888,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
       t = te;
       if (t >= ntiles) break;
       fsw_load<A_, D, SW>(src, n, t * (size_t)TE, a, nv);
-      if (single && Tr::bits(yin) == Tr::bits(Tr::round(pre[t - 1] + sums[t - 1]))) {
+      if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t - 1], sums[t - 1]))) {
         const size_t nt = fsw_next_failed(tfail, t, ntiles, ldsx);
         if (nt >= ntiles) break;
         if (nt != t) {
           t = nt;
-          yin = Tr::round(pre[nt - 1] + sums[nt - 1]);
+          yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
           fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         }
         serial_run = 0;
@@ -883,11 +916,11 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     bool go_serial = false;
     const int cap = serial_run > 0 ? FSW_PROBE_CAP : FSW_CAP;
     if (!go_serial) {
-      double p[FS_Q][W];
-      fsw_scan<V, W>(v, p, ldsq);
+      P p[FS_Q][W];
+      fsw_scan<V, W, P>(v, p, ldsq);
       // candidates c_i = D(kb + p_i) with kb = y_base - p_base (one add per
       // element; any association proposes, the check decides)
-      double kb = has_in ? (double)Tr::val(yin) : 0.0;
+      P kb = has_in ? (P)Tr::val(yin) : (P)0;
       int steps = 0;
       for (;; par ^= 1) {
         // candidates (branch-free: every element computes, selects keep the
@@ -934,7 +967,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
         // element position of that lane
         int wf = NOFAIL;
         S wv = (S)0;
-        double wp = 0.0;
+        P wp = 0;
         if (__ballot(bm != 0)) {
           int fl = 0, fk = 0;
 #pragma unroll
@@ -946,7 +979,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
             }
           }
           S r = (S)0;
-          double pk = 0.0;
+          P pk = 0;
 #pragma unroll
           for (int k = 0; k < FS_Q * W; ++k) {
             if (k == fk) {  // uniform
@@ -975,12 +1008,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
         // selected last (all LDS reads independent)
         int f = NOFAIL;
         S fv = (S)0;
-        double fp = 0.0;
+        P fp = 0;
 #pragma unroll
         for (int w = FSW_NW - 1; w >= 0; --w) {
           const int wfi = lds_fi[par][w];
           const S wfv = lds_fv[par][w], bc = lds_bc[par][w];
-          const double wfp = lds_fp[par][w], bp = lds_bp[par][w];
+          const P wfp = lds_fp[par][w], bp = lds_bp[par][w];
           const V bv = lds_bv[par][w];
           const S pe = w ? lds_last[par][w - 1] : yin;  // w = 0: only checked while fpos < 0
           f = fsw_sel(wfi != NOFAIL, wfi, f);
@@ -997,7 +1030,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
         // re-base at f: numpy's value there (its predecessor is verified)
         fpos = f;
         fixed = fv;
-        kb = (double)Tr::val(fv) - fp;
+        kb = (P)Tr::val(fv) - fp;
         if (++steps >= cap) {
           go_serial = true;
           break;
@@ -1046,13 +1079,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     has_in = true;
     fsw_store<A_, D, SW>(dst, n, t0, c);
     if (t + 1 >= ntiles) break;
-    if (single && Tr::bits(yin) == Tr::bits(Tr::round(pre[t] + sums[t]))) {
+    if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t], sums[t]))) {
       // in sync with the apply pass: tiles that verified there are final
       const size_t nt = fsw_next_failed(tfail, t + 1, ntiles, ldsx);
       if (nt >= ntiles) break;
       if (nt != t + 1) {
         t = nt;
-        yin = Tr::round(pre[nt - 1] + sums[nt - 1]);
+        yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
         fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         continue;
       }

@@ -9,3 +9,5 @@ timeout -k 10 300 python -u tools/probe_shuffle_tiles.py 4 > gpurun_out/probe_sh
 grep -E "v129|v513|mc_copy|copy_u|bad|failures" gpurun_out/probe_shuffle_tiles.log
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_default.log 2>&1 || exit $?
 tail -c 3000 gpurun_out/bench_default.log
+timeout -k 10 120 python -u tools/probe_verify_overhead.py > gpurun_out/probe_verify_overhead.log 2>&1 || exit $?
+cat gpurun_out/probe_verify_overhead.log

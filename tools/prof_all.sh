@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-CONFIGS=${*:-"C2_f32 C2_f64 C3 C4 C5 D_i2 F32 CRC32"}
+CONFIGS=${*:-"C2_f32 C2_f64 C3 C4 C5 D_i2 F32 CRC32 CRC32C ADLER32 PACKBITS ASTYPE BLOSC_S BLOSC_B FSO_LE FSO_BE DF4_LE DF4_BE DI2_BE"}
 for cfg in $CONFIGS; do
   for dir in enc dec; do
     key="${cfg}_${dir}"

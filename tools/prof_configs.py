@@ -20,6 +20,16 @@ Configs and their algorithmic HBM bytes per call:
   D_i2     Delta(<i2), 256 MiB                        2N each way
   F32      Fletcher32, 256 MiB (decode: public API)   enc 2N + 4, dec N + 4
   CRC32    CRC32, 256 MiB (decode: public API)        enc 2N + 4, dec N + 4
+  CRC32C / ADLER32   as CRC32
+  PACKBITS PackBits, 256 MiB of bools                 enc N + N/8 + 1, dec N/8 + 1 + N
+  ASTYPE   AsType(<f8 <- <f4), 256 MiB of f4          3N each way
+  BLOSC_S / BLOSC_B  Blosc SHUFFLE / BITSHUFFLE filter, typesize 4,
+           256 KiB blocks, 256 MiB                    2N each way
+  FSO_LE / FSO_BE    FixedScaleOffset(1000, 1e3, f4 -> i2), '<f4'->'<i2' and
+           '>f4'->'>i2', 256 MiB of f4                1.5N each way
+  DF4_LE / DF4_BE    Delta('<f4') / Delta('>f4'), 256 MiB of smooth f4
+           (speculative decode)                       2N each way
+  DI2_BE   Delta('>i2'), 256 MiB                      2N each way
 """
 
 import json
@@ -29,7 +39,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from numcodecs_amd import CRC32, BitRound, Delta, FixedScaleOffset, Fletcher32, Shuffle, batch  # noqa: E402
+from numcodecs_amd import (  # noqa: E402
+    CRC32, CRC32C, Adler32, AsType, BitRound, Delta, FixedScaleOffset, Fletcher32, PackBits, Shuffle, batch,
+)
+from numcodecs_amd import blosc_shuffle as bsh  # noqa: E402
 
 MiB = 1 << 20
 N = 256 * MiB
@@ -74,11 +87,48 @@ def config(name, dev):
         xs = [torch.randint(-100, 100, (N // 2,), dtype=torch.int16, device=dev) for _ in range(SETS)]
         encs = [d.encode(x) for x in xs]
         return (lambda i: d.encode(xs[i])), (lambda i: d.decode(encs[i])), 2 * N, 2 * N
-    if name in ("F32", "CRC32"):
-        c = Fletcher32() if name == "F32" else CRC32()
+    if name in ("F32", "CRC32", "CRC32C", "ADLER32"):
+        c = {"F32": Fletcher32, "CRC32": CRC32, "CRC32C": CRC32C, "ADLER32": Adler32}[name]()
         xs = [torch.randint(0, 256, (N,), dtype=torch.uint8, device=dev) for _ in range(SETS)]
         encs = [c.encode(x) for x in xs]
         return (lambda i: c.encode(xs[i])), (lambda i: c.decode(encs[i])), 2 * N + 4, N + 4
+    if name == "PACKBITS":
+        pb = PackBits()
+        xs = [torch.randint(0, 2, (N,), dtype=torch.uint8, device=dev).view(torch.bool) for _ in range(SETS)]
+        encs = [pb.encode(x) for x in xs]
+        return (lambda i: pb.encode(xs[i])), (lambda i: pb.decode(encs[i])), N + N // 8 + 1, N // 8 + 1 + N
+    if name == "ASTYPE":
+        at = AsType(encode_dtype="<f8", decode_dtype="<f4")
+        xs = [torch.randn(N // 4, device=dev) for _ in range(SETS)]
+        encs = [at.encode(x) for x in xs]
+        return (lambda i: at.encode(xs[i])), (lambda i: at.decode(encs[i])), 3 * N, 3 * N
+    if name in ("BLOSC_S", "BLOSC_B"):
+        mode = 1 if name == "BLOSC_S" else 2
+        xs = [torch.randint(0, 256, (N,), dtype=torch.uint8, device=dev) for _ in range(SETS)]
+        encs = [bsh.shuffle(x, 4, 256 * 1024, mode) for x in xs]
+        return ((lambda i: bsh.shuffle(xs[i], 4, 256 * 1024, mode)),
+                (lambda i: bsh.unshuffle(encs[i], 4, 256 * 1024, mode)), 2 * N, 2 * N)
+    if name in ("FSO_LE", "FSO_BE"):
+        bo = "<" if name == "FSO_LE" else ">"
+        f = FixedScaleOffset(offset=1000, scale=1e3, dtype=bo + "f4", astype=bo + "i2")
+        xs = [(1000.0 + 10.0 * torch.rand(N // 4, device=dev)) for _ in range(SETS)]
+        if bo == ">":  # the same values stored big-endian (raw device bytes)
+            xs = [x.view(torch.int32).view(torch.uint8).view(-1, 4).flip(1).contiguous().view(-1) for x in xs]
+        encs = [f.encode(x) for x in xs]
+        return (lambda i: f.encode(xs[i])), (lambda i: f.decode(encs[i])), 3 * N // 2, 3 * N // 2
+    if name in ("DF4_LE", "DF4_BE", "DI2_BE"):
+        if name == "DI2_BE":
+            d, es = Delta(">i2"), 2
+            xs = [torch.randint(-100, 100, (N // 2,), dtype=torch.int16, device=dev).view(torch.uint8)
+                  for _ in range(SETS)]
+        else:
+            bo = "<" if name == "DF4_LE" else ">"
+            d, es = Delta(bo + "f4"), 4
+            xs = [(torch.arange(N // 4, device=dev, dtype=torch.float64) * 0.25 % 4096.0).float() for _ in range(SETS)]
+            if bo == ">":
+                xs = [x.view(torch.uint8).view(-1, 4).flip(1).contiguous().view(-1) for x in xs]
+        encs = [d.encode(x) for x in xs]
+        return (lambda i: d.encode(xs[i])), (lambda i: d.decode(encs[i])), 2 * N, 2 * N
     raise SystemExit(f"unknown config {name}")
 
 
