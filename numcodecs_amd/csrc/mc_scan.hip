@@ -733,10 +733,22 @@ size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
   return w > two_launch ? w : two_launch;
 }
 
+// np.cumsum(enc, out=dec) accumulates in promote_types(astype, dtype); the
+// device reproduces that for a float dtype (any astype), an integer dtype
+// from an integer/bool astype (wrap-around: the same modulo 2^bits) and
+// bool from bool.  A float astype into an integer/bool dtype and an integer
+// astype into bool are not implemented (MC_EINVAL, never different bytes).
+static bool delta_decode_pair_ok(int astype, int dtype) {
+  if (mc_is_float(dtype)) return true;
+  if (mc_is_float(astype)) return false;
+  return dtype != MC_B1 || astype == MC_B1;
+}
+
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
                     size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
   if (ticket && (uintptr_t)ticket % 8) return MC_EINVAL;
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
+  if (!delta_decode_pair_ok(astype, dtype)) return MC_EINVAL;
   if (n == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;
   hipStream_t st = (hipStream_t)stream;
@@ -841,6 +853,7 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
                                mc_stream_t stream) {
   if (variant < 0 || variant > 5) return MC_EINVAL;
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
+  if (!delta_decode_pair_ok(astype, dtype)) return MC_EINVAL;
   if (n == 0 || nchunks == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;
   if (nchunks > 1 && (src_stride < n * mc_itemsize(astype) || dst_stride < n * mc_itemsize(dtype)))

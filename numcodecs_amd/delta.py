@@ -30,6 +30,23 @@ def check_first_elements(firsts, dtype, astype) -> None:
         tmp[0] = v
 
 
+def check_decode_pair(astype, dtype) -> None:
+    """np.cumsum(enc, out=dec) (delta.py:80) accepts every numeric pair: it
+    accumulates in np.promote_types(astype, dtype) and casts each running sum
+    to dtype.  The device decode reproduces that for a float dtype (any
+    astype) and for an integer dtype with an integer/bool astype (wrap-around
+    sums: accumulating in the wider integer and casting back is the same
+    modulo 2^bits) and bool from bool (logical or).  A float astype into an
+    integer/bool dtype (a float running sum, truncated per element) and an
+    integer astype into bool (a nonzero test of an integer running sum) are
+    not implemented and raise instead of returning different bytes."""
+    a, d = np.dtype(astype), np.dtype(dtype)
+    if d.kind in "iub" and a.kind == "f" or d.kind == "b" and a.kind != "b":
+        raise NotImplementedError(
+            f"Delta decode of {a.str!r} into {d.str!r} (a running sum in "
+            f"{np.promote_types(a, d).str!r} cast to {d.str!r}) is not implemented on the device")
+
+
 class Delta(Codec):
     """Store each element as its difference from the previous one (the first
     element as itself), numcodecs id ``delta``.
@@ -69,12 +86,7 @@ class Delta(Codec):
         if src.nbytes % self.astype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.astype.itemsize
-        if not np.can_cast(self.astype, self.dtype, casting="same_kind"):
-            # np.cumsum(enc, out=dec) refuses the output cast (delta.py:80)
-            raise TypeError(
-                f"Cannot cast ufunc 'add' output from {self.astype!r} to {self.dtype!r} "
-                "with casting rule 'same_kind'"
-            )
+        check_decode_pair(self.astype, self.dtype)
         direct = device_out_bytes(out, n * self.dtype.itemsize, src)
         dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
         _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)

@@ -224,3 +224,23 @@ def test_is_ndarray_like_mirrors_reference_protocol():
     assert not is_ndarray_like(b"abc")
     assert not is_ndarray_like(bytearray(3))
     assert not is_ndarray_like(memoryview(b"abc"))
+
+
+def test_delta_decode_pairs():
+    """np.cumsum(enc, out=dec) (delta.py:80) accepts every numeric pair (it
+    accumulates in promote_types(astype, dtype)); the device covers float
+    dtypes, integer-from-integer (wrap-around) and bool-from-bool, and
+    refuses the two families whose running sum it does not reproduce."""
+    import itertools
+
+    from numcodecs_amd.delta import check_decode_pair
+
+    ts = ["|b1", "|i1", "<i2", ">i4", "<i8", "|u1", ">u2", "<u4", "<u8", "<f2", ">f4", "<f8"]
+    for a, d in itertools.product(ts, ts):
+        ka, kd = np.dtype(a).kind, np.dtype(d).kind
+        refused = (kd in "iub" and ka == "f") or (kd == "b" and ka != "b")
+        if refused:
+            with pytest.raises(NotImplementedError):
+                check_decode_pair(a, d)
+        else:
+            check_decode_pair(a, d)
