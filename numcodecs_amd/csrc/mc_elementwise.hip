@@ -474,7 +474,9 @@ int mc_bitround(const void *src, void *dst, size_t n, int itemsize, int keepbits
 
 int mc_cast(const void *src, void *dst, size_t n, int from_dtype, int to_dtype,
             mc_stream_t stream) {
-  MapParams p{from_dtype, from_dtype, from_dtype, to_dtype, McNum{0, 0}, McNum{0, 0}};
+  // compute dtypes are native: the byte order lives in the input/output codes
+  const int fb = mc_dt_base(from_dtype);
+  MapParams p{from_dtype, fb, fb, to_dtype, McNum{0, 0}, McNum{0, 0}};
   return launch_map<K_CAST>(src, dst, n, p, (hipStream_t)stream);
 }
 
@@ -501,7 +503,8 @@ int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3, int 
 int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, double scale,
                 mc_stream_t stream) {
   if (!mc_is_float(dtype) || !mc_is_float(astype)) return MC_EINVAL;
-  MapParams p{dtype, dtype, dtype, astype, num_scalar(dtype, scale, 0), McNum{0, 0}};
+  const int db = mc_dt_base(dtype);  // the computation's dtype (native)
+  MapParams p{dtype, db, db, astype, num_scalar(dtype, scale, 0), McNum{0, 0}};
   return launch_map<K_QUANTIZE>(src, dst, n, p, (hipStream_t)stream);
 }
 
