@@ -292,10 +292,21 @@ MC_DEV uint32_t swar_sub(uint32_t a, uint32_t b) {
   }
 }
 
-template <int ES>
+template <int ES, bool FL = false>
 MC_DEV mc_u32x4 delta_vec(mc_u32x4 x, uint32_t p_lo, uint32_t p_hi) {
   // p_hi:p_lo = the 8 bytes just before x (p_hi the dword right before x.x)
-  if constexpr (ES == 8) {
+  if constexpr (FL && ES == 8) {  // f8: IEEE double differences (numpy's f8 subtract)
+    const double a0 = mc_bits_f64(((uint64_t)x.y << 32) | x.x), a1 = mc_bits_f64(((uint64_t)x.w << 32) | x.z);
+    const double b0 = mc_bits_f64(((uint64_t)p_hi << 32) | p_lo);
+    const uint64_t r0 = mc_f64_bits(mc_x86_nan(a0, b0, a0 - b0)), r1 = mc_f64_bits(mc_x86_nan(a1, a0, a1 - a0));
+    return mc_u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+  } else if constexpr (FL) {  // f4: IEEE float differences
+    static_assert(ES == 4, "float same-type Delta encode: f4 / f8");
+    const float a0 = mc_bits_f32(x.x), a1 = mc_bits_f32(x.y), a2 = mc_bits_f32(x.z), a3 = mc_bits_f32(x.w);
+    const float b0 = mc_bits_f32(p_hi);
+    return mc_u32x4{mc_f32_bits(mc_x86_nan(a0, b0, a0 - b0)), mc_f32_bits(mc_x86_nan(a1, a0, a1 - a0)),
+                    mc_f32_bits(mc_x86_nan(a2, a1, a2 - a1)), mc_f32_bits(mc_x86_nan(a3, a2, a3 - a2))};
+  } else if constexpr (ES == 8) {
     const uint64_t a0 = ((uint64_t)x.y << 32) | x.x, a1 = ((uint64_t)x.w << 32) | x.z;
     const uint64_t b0 = ((uint64_t)p_hi << 32) | p_lo;
     const uint64_t r0 = a0 - b0, r1 = a1 - a0;
@@ -314,8 +325,9 @@ MC_DEV mc_u32x4 delta_vec(mc_u32x4 x, uint32_t p_lo, uint32_t p_hi) {
 }
 
 // SW: bit 0 = the input is big-endian, bit 1 = the output is (the bytes of
-// each element reversed after the load / before the store, v_perm_b32)
-template <int ES, int SW = 0>
+// each element reversed after the load / before the store, v_perm_b32).
+// FL: f4 / f8 (float differences; the first element is copied as it is).
+template <int ES, int SW = 0, bool FL = false>
 __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__restrict__ src,
                                                              uint8_t *__restrict__ dst, size_t nbytes,
                                                              size_t src_stride, size_t dst_stride) {
@@ -352,7 +364,11 @@ __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__re
     const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
     // the previous 8 bytes: lane - 1's last dwords, lane 0's read above
     const uint32_t p_hi = mc_wave_shr1(x[r].w, q_hi[r]), p_lo = mc_wave_shr1(x[r].z, q_lo[r]);
-    mc_u32x4 y = delta_vec<ES>(x[r], p_lo, p_hi);
+    mc_u32x4 y = delta_vec<ES, FL>(x[r], p_lo, p_hi);
+    if (FL && off == 0) {  // element 0 is stored as itself (x - 0 would turn -0.0 into +0.0)
+      y.x = x[r].x;
+      if constexpr (ES == 8) y.y = x[r].y;
+    }
     if constexpr ((SW & 2) != 0) y = mc_bswap_vec<ES>(y);  // big-endian output
     if (off + 16 <= nbytes) {
       mc_st16<true>(dst + off, y);
@@ -433,14 +449,14 @@ static McNum num_scalar(int dt, double f, int64_t i) {
   return r;
 }
 
-template <int ES>
+template <int ES, bool FL = false>
 static void launch_delta_same(int sw, dim3 g, const uint8_t *s, uint8_t *d, size_t nbytes, size_t ss, size_t ds,
                               hipStream_t st) {
   switch (sw) {
-    case 0: k_delta_enc_same<ES, 0><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    case 1: k_delta_enc_same<ES, 1><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    case 2: k_delta_enc_same<ES, 2><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    default: k_delta_enc_same<ES, 3><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 0: k_delta_enc_same<ES, 0, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 1: k_delta_enc_same<ES, 1, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 2: k_delta_enc_same<ES, 2, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    default: k_delta_enc_same<ES, 3, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
   }
 }
 
@@ -542,7 +558,12 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
     const int db = mc_dt_base(dtype), ab = mc_dt_base(astype);
     const int sw = (mc_dt_swapped(dtype) ? 1 : 0) | (mc_dt_swapped(astype) ? 2 : 0);
     const int same = (db == ab && db != MC_B1 && !mc_is_float(db)) ? ss : 0;
-    if (same && al16 && delta_enc_vec_enabled()) {
+    if (al16 && db == ab && (db == MC_F4 || db == MC_F8)) {  // float same-type: IEEE differences
+      const size_t per = (size_t)DE_V * 16 * MC_BLOCK;
+      const dim3 g2((unsigned)((n * ss + per - 1) / per), grid.y);
+      if (db == MC_F4) launch_delta_same<4, true>(sw, g2, sc, dc, n * 4, src_stride, dst_stride, st);
+      else launch_delta_same<8, true>(sw, g2, sc, dc, n * 8, src_stride, dst_stride, st);
+    } else if (same && al16 && delta_enc_vec_enabled()) {
       const size_t per = (size_t)DE_V * 16 * MC_BLOCK;
       const dim3 g2((unsigned)((n * ss + per - 1) / per), grid.y);
       if (same == 1) k_delta_enc_same<1><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n, src_stride, dst_stride);

@@ -321,6 +321,18 @@ MC_DEV uint64_t fs_check(const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W],
   return first;
 }
 
+// the wave's smallest failing index (~0 if none): one ballot when no lane
+// failed (the common case of smooth data), the min-reduction otherwise
+MC_DEV uint64_t fs_wave_min_fail(uint64_t first) {
+  if (__builtin_amdgcn_ballot_w64(first != ~(uint64_t)0) == 0) return ~(uint64_t)0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(first, off, 64);
+    first = o < first ? o : first;
+  }
+  return first;
+}
+
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n, int a,
                                                           double *__restrict__ sums) {
@@ -380,11 +392,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   }
   uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
   fs_store<A_, D, SW>(dst, n, t0, c);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t o = __shfl_xor(first, off, 64);
-    first = o < first ? o : first;
-  }
+  first = fs_wave_min_fail(first);
   if (lane == 0 && first != ~(uint64_t)0) {
     atomicMin((unsigned long long *)(tfail + tile), (unsigned long long)first);
     atomicMin((unsigned long long *)fail, (unsigned long long)first);
@@ -445,12 +453,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_rows(const uint8_t *__restri
       else if (wave) p0[q] = ldsc[par][q][wave - 1];
       else p0[q] = q ? ldsc[par][q - 1][MC_BLOCK / 64 - 1] : prevc;
     }
-    uint64_t first = fs_check<A_, D>(c, v, p0, t0, n);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint64_t o = __shfl_xor(first, off, 64);
-      first = o < first ? o : first;
-    }
+    const uint64_t first = fs_wave_min_fail(fs_check<A_, D>(c, v, p0, t0, n));
     if (lane == 0) ldsf[par][wave] = first;
     if (threadIdx.x == MC_BLOCK - 1) ldsp[par] = carry + p[FS_Q - 1][W - 1];
     __syncthreads();
@@ -511,16 +514,22 @@ constexpr int FSW_PROBE_MAX = 64;  // the gap up to this (noise costs ~0.5 % ove
 constexpr int FSW_G = 32;          // serial chain: values per LDS read group (8 x 16 B in flight)
 constexpr int FSW_NW = MC_BLOCK / 64;
 
-// The serial chain over p[j..cnt) in place (acc = the value before p[j]),
-// numpy's order: two read groups alternate so the next group's LDS reads are
-// in flight while the current group's adds run (as in k_scan_serial).  p is
-// padded by 2 groups past cnt.
-template <int D>
-MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt, typename SerAcc<D>::T acc) {
+// The serial chain over p[j..cnt) (acc = the value before p[j]), numpy's
+// order: two read groups alternate so the next group's LDS reads are in
+// flight while the current group's adds run (as in k_scan_serial).  p is
+// padded by 2 groups past cnt.  OUTG = false writes the results back into p;
+// OUTG = true writes them straight to global memory at out[j..cnt) (the
+// value type is the stored type: f4 / f8 little-endian), which takes the
+// chain lane's LDS writes off its critical path -- measured 13.1 -> 11.0
+// cycles per element for the chain alone (tools/probe_chain.py kinds 1, 14).
+template <int D, bool OUTG = false>
+MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt, typename SerAcc<D>::T acc,
+                                       typename SerAcc<D>::T *out = nullptr) {
   using T = typename SerAcc<D>::T;
+  T *o = OUTG ? out : p;
   for (; j < cnt && (j & (FSW_G - 1)); ++j) {
     acc = ser_add<D>(acc, p[j]);
-    p[j] = acc;
+    o[j] = acc;
   }
   if (j + 2 * FSW_G <= cnt) {
     T ga[FSW_G], gb[FSW_G];
@@ -533,7 +542,7 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
         acc = ser_add<D>(acc, ga[k]);
         ga[k] = acc;
       }
-      ser_st<T, FSW_G>(p + j, ga);
+      ser_st<T, FSW_G>(o + j, ga);
       ser_ld<T, FSW_G>(p + j + 2 * FSW_G, ga);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -541,12 +550,12 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
         acc = ser_add<D>(acc, gb[k]);
         gb[k] = acc;
       }
-      ser_st<T, FSW_G>(p + j + FSW_G, gb);
+      ser_st<T, FSW_G>(o + j + FSW_G, gb);
     }
   }
   for (; j < cnt; ++j) {
     acc = ser_add<D>(acc, p[j]);
-    p[j] = acc;
+    o[j] = acc;
   }
   return acc;
 }
@@ -728,6 +737,9 @@ MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_
   constexpr int TE = (int)fs_tile<D>();
   constexpr int NV = TE / W;  // vectors per tile
   const int wave = threadIdx.x >> 6;
+  // same-type little-endian f4 / f8: the chain lane stores its results to
+  // dst itself (fsw_chain<D, true>); the I/O waves only load
+  constexpr bool DIRECT = A_ == D && SW == 0 && D != MC_F2;
   // the I/O waves issue FSW_IOV vector loads before the first use (one at a
   // time, each waited for, the next tile's 16 KiB took longer than the
   // chain's tile and the chain lane idled at the barrier: noise-like data
@@ -801,21 +813,24 @@ MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_
         const int cnt = (int)(n - t0 < (size_t)TE ? n - t0 : (size_t)TE);
         V *p = xs[t & 1];
         int j = 0;
+        V *out = reinterpret_cast<V *>(dst + t0 * sizeof(S));
         if (t0 == 0 && !has_in) {  // the chunk's first element: out[0] = enc[0]
           acc = p[0];
+          if constexpr (DIRECT) out[0] = acc;
           j = 1;
         }
-        acc = fsw_chain<D>(p, j, cnt, acc);
+        if constexpr (DIRECT) acc = fsw_chain<D, true>(p, j, cnt, acc, out);
+        else acc = fsw_chain<D>(p, j, cnt, acc);
         if (t + 1 == te) *ldsy = Tr::store(acc);
       }
     } else {
       const int io = threadIdx.x - 64;
-      if (t > tb) io_store(t - 1, xs[(t - 1) & 1], io, MC_BLOCK - 64);
+      if (!DIRECT && t > tb) io_store(t - 1, xs[(t - 1) & 1], io, MC_BLOCK - 64);
       if (t + 1 < te) io_load(t + 1, xs[(t + 1) & 1], io, MC_BLOCK - 64);
     }
     __syncthreads();
   }
-  io_store(te - 1, xs[(te - 1) & 1], threadIdx.x, MC_BLOCK);
+  if (!DIRECT) io_store(te - 1, xs[(te - 1) & 1], threadIdx.x, MC_BLOCK);
   const S y = *ldsy;
   __syncthreads();  // the buffers and ldsy are free again
   return y;

@@ -116,6 +116,25 @@ MC_DEV McNum mc_num_cast(McNum v, int from, int to) {
 
 enum McOp { MC_OP_ADD, MC_OP_SUB, MC_OP_MUL, MC_OP_DIV };
 
+// The NaN an x86-64 SSE add/sub/mul/div returns (numpy's float loops): the
+// first operand's NaN quieted, else the second's, else -- an invalid
+// operation such as inf - inf -- the negative "real indefinite" quiet NaN.
+// The GPU computes x - y as x + (-y), which flips the sign of a NaN y, and
+// its default NaN is positive; non-NaN results are the same IEEE values.
+template <typename F>
+MC_DEV F mc_x86_nan(F x, F y, F r) {
+  if (!__builtin_isnan(r)) return r;
+  if constexpr (sizeof(F) == 8) {
+    constexpr uint64_t Q = 1ull << 51, DEF = 0xFFF8000000000000ull;
+    const uint64_t b = __builtin_isnan(x) ? mc_f64_bits(x) | Q : __builtin_isnan(y) ? mc_f64_bits(y) | Q : DEF;
+    return mc_bits_f64(b);
+  } else {
+    constexpr uint32_t Q = 1u << 22, DEF = 0xFFC00000u;
+    const uint32_t b = __builtin_isnan(x) ? mc_f32_bits(x) | Q : __builtin_isnan(y) ? mc_f32_bits(y) | Q : DEF;
+    return mc_bits_f32(b);
+  }
+}
+
 // a <op> b with both operands already in dtype dt
 MC_DEV McNum mc_num_binop(McNum a, McNum b, int op, int dt) {
   dt = mc_dt_base(dt);
@@ -127,7 +146,7 @@ MC_DEV McNum mc_num_binop(McNum a, McNum b, int op, int dt) {
       case MC_OP_MUL: r = a.f * b.f; break;
       default: r = a.f / b.f; break;
     }
-    return mc_num_f(r);
+    return mc_num_f(mc_x86_nan(a.f, b.f, r));
   }
   if (dt == MC_F4 || dt == MC_F2) {
     const float x = (float)a.f, y = (float)b.f;
@@ -138,6 +157,7 @@ MC_DEV McNum mc_num_binop(McNum a, McNum b, int op, int dt) {
       case MC_OP_MUL: r = x * y; break;
       default: r = x / y; break;
     }
+    r = mc_x86_nan(x, y, r);
     if (dt == MC_F2) r = mc_half_to_float(mc_float_to_half(r));
     return mc_num_f((double)r);
   }

@@ -117,26 +117,32 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
     }
   };
 
+  // same-type little-endian f4 / f8 with vector access: the chain lane
+  // stores its results straight to dst (16-B global stores), the I/O wave
+  // only loads -- the chain's LDS writes were on its critical path (13.1 ->
+  // 11.0 cycles per element, tools/probe_chain.py kinds 1 and 14)
+  constexpr bool DIRECT = L == D && A_ == D && VEC && !SWO && D != MC_F2;
   if (io) load_blk(0);
   __syncthreads();
   T acc = 0;
   for (size_t b = 0; b < nb; ++b) {
     if (io) {
-      if (b >= 1) store_blk(b - 1);
+      if (!DIRECT && b >= 1) store_blk(b - 1);
       if (b + 1 < nb) load_blk(b + 1);
     } else if (lane == 0) {
       // software-pipelined chain: group g+1's LDS reads are in flight while
       // group g's adds run (ds_read latency ~50 cycles vs ~G dependent adds)
       T *p = slot[b & 1];
+      T *o = DIRECT ? reinterpret_cast<T *>(dst + b * BLK * (size_t)DS) : p;
       const int cnt = (int)min((size_t)BLK, n - b * BLK);
       int j = 0;
       if (b == 0) {  // out[0] = x[0] exactly (no add), then align to a group
         acc = has_carry ? ser_add<L>(carry, p[0]) : p[0];
-        p[0] = acc;
+        o[0] = acc;
         const int m = cnt < SER_G ? cnt : SER_G;
         for (int k = 1; k < m; ++k) {
           acc = ser_add<L>(acc, p[k]);
-          p[k] = acc;
+          o[k] = acc;
         }
         j = m;
       }
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
             acc = ser_add<L>(acc, ga[k]);
             ga[k] = acc;
           }
-          ser_st<T, SER_G>(p + j, ga);
+          ser_st<T, SER_G>(o + j, ga);
           ser_ld<T, SER_G>(p + j + 2 * SER_G, ga);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -162,17 +168,17 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
             acc = ser_add<L>(acc, gb[k]);
             gb[k] = acc;
           }
-          ser_st<T, SER_G>(p + j + SER_G, gb);
+          ser_st<T, SER_G>(o + j + SER_G, gb);
         }
       }
       for (; j < cnt; ++j) {
         acc = ser_add<L>(acc, p[j]);
-        p[j] = acc;
+        o[j] = acc;
       }
     }
     __syncthreads();
   }
-  if (io) store_blk(nb - 1);
+  if (io && !DIRECT) store_blk(nb - 1);
 }
 
 // (slot bytes, group) per schedule: a 32 KiB slot amortises the block

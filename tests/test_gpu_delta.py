@@ -214,3 +214,67 @@ def test_two_launch_int_decode_vs_oracle(device, dt, n):
     assert torch.equal(out.view(torch.uint8), dec.reshape(-1).view(torch.uint8))
     torch.cuda.synchronize()
     assert not _ops._verify_slot(src, _ops.stream(src)).ticket.any()
+
+
+def _special_floats(dt, n, seed):
+    """normal values with NaNs of several payloads (quiet and signalling),
+    infinities, signed zeros and subnormals sprinkled in."""
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dt)
+    x = rng.normal(0, 3, n).astype(dt)
+    if n < 4:
+        return x
+    bits = x.view(np.dtype((">" if dt.byteorder == ">" else "<") + f"u{dt.itemsize}"))
+    nan_bits = [0x7FC00001, 0xFFC12345, 0x7F800001] if dt.itemsize == 4 else [
+        0x7FF8000000000001, 0xFFF0000000000ABC, 0x7FF0000000000001]
+    tiny = np.finfo(dt).tiny
+    special = [np.inf, -np.inf, -0.0, 0.0, tiny / 8, -tiny / 3]
+    for i, k in enumerate(rng.choice(n, min(n, 24), replace=False)):
+        if i % 3 == 0:
+            bits[k] = nan_bits[(i // 3) % 3]
+        else:
+            x[k] = special[i % len(special)]
+    return x
+
+
+@pytest.mark.parametrize("dt", ["<f4", ">f4", "<f8", ">f8"])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 63, 4096, 4097, 65536 + 3, 262144 * 3 + 7])
+def test_float_delta_encode_same_type_special_values(device, dt, n):
+    """Same-type float Delta encode (the 16-B vector kernel, byte swaps fused
+    for big-endian): IEEE differences in dtype, numpy's bytes for NaNs,
+    infinities, signed zeros and subnormals, at every tile boundary."""
+    x = _special_floats(dt, n, n)
+
+    def enc_bytes(a):  # raw device bytes in (torch holds no big-endian dtypes), bytes out
+        out = Delta(dt).encode(torch.from_numpy(a.view(np.uint8).copy()).to(device))
+        return out.contiguous().view(torch.uint8).cpu().numpy().tobytes()
+
+    assert enc_bytes(x) == _oracle_enc(x, dt, dt).tobytes(), (dt, n)
+    x[0] = -0.0  # the first element is stored as it is (never 0 - x)
+    assert enc_bytes(x) == _oracle_enc(x, dt, dt).tobytes(), (dt, n)
+
+
+@pytest.mark.parametrize("dt", ["<f2", "<f4", "<f8", ">f4"])
+@pytest.mark.parametrize("n", [7, 5000, 70001])
+def test_float_delta_decode_nan_payloads(device, dt, n):
+    """numpy's cumsum keeps the first NaN's payload (x86: the first operand's
+    NaN, quieted) and gives inf + -inf the negative default NaN: the device
+    decode returns the same bytes."""
+    rng = np.random.default_rng(n)
+    d = np.dtype(dt)
+    x = rng.normal(0, 1, n).astype(d)
+    ub = np.dtype((">" if d.byteorder == ">" else "<") + f"u{d.itemsize}")
+    pay = {2: [0x7E01, 0xFE35, 0x7C01], 4: [0x7FC00001, 0xFFC12345, 0x7F800001],
+           8: [0x7FF8000000000001, 0xFFF0000000000ABC, 0x7FF0000000000001]}[d.itemsize]
+    k = max(1, n // 3)
+    x.view(ub)[k] = pay[n % 3]
+    if n > 10:
+        x.view(ub)[k + 1] = pay[(n + 1) % 3]  # a second NaN after the first
+    dec = Delta(dt).decode(torch.from_numpy(x.view(np.uint8).copy()).to(device))
+    got = dec.contiguous().view(torch.uint8).cpu().numpy().tobytes()
+    assert got == _oracle_dec(x, dt, dt).tobytes()
+    y = rng.normal(0, 1, n).astype(d)
+    y[k] = np.inf
+    y[-1] = -np.inf
+    dec = Delta(dt).decode(torch.from_numpy(y.view(np.uint8).copy()).to(device))
+    assert dec.contiguous().view(torch.uint8).cpu().numpy().tobytes() == _oracle_dec(y, dt, dt).tobytes()

@@ -14,6 +14,37 @@
 //   kind 4  DPP-fed adds: lanes 0-15 load 64 values with one ds_read_b128
 //           each, lane 0 adds them through v_add_f32 with a row_shl source
 //           (no per-element move), results written by lane 0 as 16-B stores
+//   kinds 5-10  NS register sets of G values rotating (k_lab_chain_rot):
+//           group t's adds, the store of group t-1 (computed a whole group
+//           earlier, so the store never waits on its data and nothing
+//           overwrites its registers soon after), the load of group t+NS-2
+//           into the set stored one step ago.  ORD 0 = adds first, ORD 1 =
+//           store + load first.  5: G16 NS4, 6: G16 NS8, 7: G32 NS4,
+//           8: G16 NS4 ORD1, 9: G8 NS8, 10: G16 NS8 ORD1
+//   kinds 11-15  SGPR-fed chain (k_lab_chain_sgpr): the inputs come from
+//           global memory through scalar loads (constant address space), so
+//           the adds read SGPR operands and no input passes through VGPRs;
+//           the chain runs in every lane (uniform).  11: no result stores,
+//           12: lane 0 writes the results to LDS (ds_write_b128), 13: lane 0
+//           writes them to global memory (16-B stores), 14: kind 1's LDS-fed
+//           chain with global result stores, 15: SGPR-fed, results gathered
+//           into lane k of a VGPR (v_cndmask per element) and written as one
+//           wave-wide 4-B store per 64 elements
+//   kinds 16-18  kind 13 run redundantly by WAVES waves (one per SIMD): every
+//           wave computes the whole chain, wave w stores only the 32-value
+//           groups g with g % WAVES == w, so each wave's store cost per
+//           element drops by WAVES.  16: 4 waves, 17: 2 waves, 18: 8 waves
+//   kinds 19-21  kind 13 variants: 19 stores only every 16th group (is it
+//           the stores or the distinct result registers?), 20 stores each
+//           value with its own 4-B store, 21 stores a group only after the
+//           next group's adds (two result sets alternate)
+//   kinds 22-23  the chain values are the same in every lane, so every lane
+//           stores them (same addresses, no lane-0 branch that lets the
+//           compiler sink the adds past the stores): 22 = kind 21's lagging
+//           stores, 23 = kind 13's
+//   kinds 24-25  kind 1 / kind 14 (LDS-fed) run by all 64 lanes of the wave
+//           (uniform chain, broadcast LDS reads, same-address stores): 24
+//           writes the results back to LDS, 25 to global memory
 #include "mc_scan.h"
 
 namespace {
@@ -66,8 +97,8 @@ __global__ __launch_bounds__(64) void k_lab_chain(const float *__restrict__ init
           v[j & 15] = acc;
         }
     }
-  } else if constexpr (KIND == 1 || KIND == 3) {
-    if (threadIdx.x == 0) {
+  } else if constexpr (KIND == 1 || KIND == 3 || KIND == 24) {
+    if (KIND == 24 || threadIdx.x == 0) {
       for (int r = 0; r < reps; ++r) {
         float ga[CG], gb[CG];
         ser_ld<float, CG>(p, ga);
@@ -79,7 +110,7 @@ __global__ __launch_bounds__(64) void k_lab_chain(const float *__restrict__ init
             acc = acc + ga[k];
             ga[k] = acc;
           }
-          if constexpr (KIND == 1) ser_st<float, CG>(p + j, ga);
+          if constexpr (KIND != 3) ser_st<float, CG>(p + j, ga);
           ser_ld<float, CG>(p + j + 2 * CG, ga);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -87,7 +118,7 @@ __global__ __launch_bounds__(64) void k_lab_chain(const float *__restrict__ init
             acc = acc + gb[k];
             gb[k] = acc;
           }
-          if constexpr (KIND == 1) ser_st<float, CG>(p + j + CG, gb);
+          if constexpr (KIND != 3) ser_st<float, CG>(p + j + CG, gb);
           else acc += gb[0] * 0.0f;
         }
       }
@@ -162,11 +193,261 @@ __global__ __launch_bounds__(64) void k_lab_chain(const float *__restrict__ init
   }
 }
 
+template <int G, int NS, int ORD>
+__global__ __launch_bounds__(64) void k_lab_chain_rot(const float *__restrict__ init, float *__restrict__ out,
+                                                     long long *__restrict__ cyc, int n, int reps) {
+  __shared__ __attribute__((aligned(16))) float p[8192 + 4 * CG];
+  for (int i = threadIdx.x; i < n + 4 * CG; i += 64) p[i] = init[i % 64];
+  __syncthreads();
+  float acc = 0.0f;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    constexpr int P = NS - 2;  // prefetch distance in groups
+    float s[NS][G];
+    const int mask = n - 1;    // n is a power of two
+#pragma unroll
+    for (int u = 0; u < P; ++u) ser_ld<float, G>(p + u * G, s[u]);
+    int base = 0;
+    const int steps = (n / G) * reps;
+    for (int t = 0; t < steps; t += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        float(&cur)[G] = s[u];
+        float(&prev)[G] = s[(u + NS - 1) % NS];
+        float(&nxt)[G] = s[(u + P) % NS];
+        const int pa = (base - G) & mask, la = (base + P * G) & mask;
+        if constexpr (ORD == 1) {
+          if (t + u > 0) ser_st<float, G>(p + pa, prev);
+          ser_ld<float, G>(p + la, nxt);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          acc = acc + cur[k];
+          cur[k] = acc;
+        }
+        if constexpr (ORD == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + u > 0) ser_st<float, G>(p + pa, prev);
+          ser_ld<float, G>(p + la, nxt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        base = (base + G) & mask;
+      }
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    out[0] = acc + p[7];
+    cyc[0] = t1 - t0;
+  }
+}
+
+typedef const __attribute__((address_space(4))) float *cfp;
+
+template <int KIND, int WAVES = 1>
+__global__ __launch_bounds__(64 * WAVES) void k_lab_chain_sgpr(const float *__restrict__ init, float *__restrict__ out,
+                                                      long long *__restrict__ cyc, int n, int reps,
+                                                      const float *__restrict__ gin, float *__restrict__ gout) {
+  __shared__ __attribute__((aligned(16))) float p[8192 + 4 * CG];
+  for (int i = threadIdx.x; i < n + 4 * CG; i += 64 * WAVES) p[i] = init[i % 64];
+  __syncthreads();
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float acc = 0.0f;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  if constexpr (KIND == 14 || KIND == 25) {
+    if (KIND == 25 || lane == 0) {
+      for (int r = 0; r < reps; ++r) {
+        float ga[CG], gb[CG];
+        ser_ld<float, CG>(p, ga);
+        for (int j = 0; j + 2 * CG <= n; j += 2 * CG) {
+          ser_ld<float, CG>(p + j + CG, gb);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < CG; ++k) {
+            acc = acc + ga[k];
+            ga[k] = acc;
+          }
+          ser_st<float, CG>(gout + j, ga);
+          ser_ld<float, CG>(p + j + 2 * CG, ga);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < CG; ++k) {
+            acc = acc + gb[k];
+            gb[k] = acc;
+          }
+          ser_st<float, CG>(gout + j + CG, gb);
+        }
+      }
+    }
+  } else if constexpr (KIND == 21 || KIND == 22) {
+    cfp src = (cfp)gin;
+    constexpr int SG = 32;
+    auto sld = [&](int at, float (&g)[SG]) {
+#pragma unroll
+      for (int k = 0; k < SG; ++k) g[k] = src[at + k];
+    };
+    auto st = [&](int at, const float (&r)[SG]) {
+      if (KIND == 22 || lane == 0) {
+#pragma unroll
+        for (int k = 0; k < SG / 4; ++k)
+          reinterpret_cast<f4v *>(gout + at)[k] = f4v{r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]};
+      }
+    };
+    if constexpr (KIND == 21) {
+      for (int r = 0; r < reps; ++r) {
+        float ga[SG], gb[SG], ra[SG], rb[SG];
+        sld(0, ga);
+#pragma unroll
+        for (int k = 0; k < SG; ++k) rb[k] = 0.0f;
+        for (int j = 0; j < n; j += 2 * SG) {
+          const int jj = __builtin_amdgcn_readfirstlane(j);
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_sched_barrier(0);
+          sld(jj + SG, gb);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < SG; ++k) {
+            acc = acc + ga[k];
+            ra[k] = acc;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          st((jj - SG) & (n - 1), rb);  // the previous group, computed a group ago
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          __builtin_amdgcn_sched_barrier(0);
+          sld((jj + 2 * SG) & (n - 1), ga);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < SG; ++k) {
+            acc = acc + gb[k];
+            rb[k] = acc;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          st(jj, ra);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      // 4 result sets: group t writes S[t % 4], the stores of S[(t-1) % 4]
+      // follow its adds, and S[(t-2) % 4] is kept alive (empty asm use) until
+      // after them, so no add ever writes a register a store issued less
+      // than a whole group earlier may still be reading
+      for (int r = 0; r < reps; ++r) {
+        float G[2][SG], S[4][SG];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int k = 0; k < SG; ++k) S[u][k] = 0.0f;
+        sld(0, G[0]);
+        for (int j = 0; j < n; j += 4 * SG) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int jj = __builtin_amdgcn_readfirstlane(j + u * SG);
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_sched_barrier(0);
+            sld((jj + SG) & (n - 1), G[(u + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < SG; ++k) {
+              acc = acc + G[u & 1][k];
+              S[u][k] = acc;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            st((jj - SG) & (n - 1), S[(u + 3) & 3]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < SG; ++k) asm volatile("" ::"v"(S[(u + 2) & 3][k]));
+          }
+        }
+      }
+    }
+  } else {
+    cfp src = (cfp)gin;
+    constexpr int SG = 32;  // SGPR group: two alternate, the next one's scalar loads in flight
+    auto sld = [&](int at, float (&g)[SG]) {
+#pragma unroll
+      for (int k = 0; k < SG; ++k) g[k] = src[at + k];
+    };
+    auto group = [&](int j, const float (&g)[SG], float &gat, int k0) {
+      float res[SG];
+#pragma unroll
+      for (int k = 0; k < SG; ++k) {
+        acc = acc + g[k];
+        if constexpr (KIND == 15) gat = lane == k0 + k ? acc : gat;
+        else res[k] = acc;
+      }
+      if constexpr (KIND == 12) {
+        if (lane == 0) {
+#pragma unroll
+          for (int k = 0; k < SG / 4; ++k)
+            reinterpret_cast<f4v *>(p + j)[k] = f4v{res[4 * k], res[4 * k + 1], res[4 * k + 2], res[4 * k + 3]};
+        }
+      } else if constexpr (KIND == 19) {
+        if (lane == 0 && (j & (16 * SG - 1)) == 0) {
+#pragma unroll
+          for (int k = 0; k < SG / 4; ++k)
+            reinterpret_cast<f4v *>(gout + j)[k] = f4v{res[4 * k], res[4 * k + 1], res[4 * k + 2], res[4 * k + 3]};
+        }
+      } else if constexpr (KIND == 20) {
+        if (lane == 0) {
+#pragma unroll
+          for (int k = 0; k < SG; ++k) gout[j + k] = res[k];
+        }
+      } else if constexpr (KIND == 23) {
+#pragma unroll
+        for (int k = 0; k < SG / 4; ++k)
+          reinterpret_cast<f4v *>(gout + j)[k] = f4v{res[4 * k], res[4 * k + 1], res[4 * k + 2], res[4 * k + 3]};
+      } else if constexpr (KIND == 13) {
+        if (lane == 0 && (WAVES == 1 || ((j / SG) % WAVES) == wave)) {
+#pragma unroll
+          for (int k = 0; k < SG / 4; ++k)
+            reinterpret_cast<f4v *>(gout + j)[k] = f4v{res[4 * k], res[4 * k + 1], res[4 * k + 2], res[4 * k + 3]};
+        }
+      } else {
+        (void)res;
+      }
+    };
+    for (int r = 0; r < reps; ++r) {
+      float ga[SG], gb[SG];
+      sld(0, ga);
+      for (int j = 0; j < n; j += 2 * SG) {
+        const int jj = __builtin_amdgcn_readfirstlane(j);
+        float gat = 0.0f;
+        // SMEM returns out of order, so any wait is lgkmcnt(0): wait for the
+        // current group first, then issue the next group's loads
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        sld(jj + SG, gb);
+        __builtin_amdgcn_sched_barrier(0);
+        group(jj, ga, gat, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        sld((jj + 2 * SG) & (n - 1), ga);
+        __builtin_amdgcn_sched_barrier(0);
+        group(jj + SG, gb, gat, SG);
+        if constexpr (KIND == 15) gout[jj + lane] = gat;
+      }
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    out[0] = acc + p[7];
+    cyc[0] = t1 - t0;
+  }
+}
+
 }  // namespace
 
 extern "C" int mc_lab_chain(const float *init, float *out, long long *cyc, int n, int reps, int kind,
                             mc_stream_t stream) {
   if (n <= 0 || n > 8192 || n % 128 || reps <= 0) return MC_EINVAL;
+  if (kind >= 5 && (n & (n - 1))) return MC_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   switch (kind) {
     case 0: k_lab_chain<0><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
@@ -174,6 +455,38 @@ extern "C" int mc_lab_chain(const float *init, float *out, long long *cyc, int n
     case 2: k_lab_chain<2><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
     case 3: k_lab_chain<3><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
     case 4: k_lab_chain<4><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 24: k_lab_chain<24><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 5: k_lab_chain_rot<16, 4, 0><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 6: k_lab_chain_rot<16, 8, 0><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 7: k_lab_chain_rot<32, 4, 0><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 8: k_lab_chain_rot<16, 4, 1><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 9: k_lab_chain_rot<8, 8, 0><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    case 10: k_lab_chain_rot<16, 8, 1><<<1, 64, 0, st>>>(init, out, cyc, n, reps); break;
+    default: return MC_EINVAL;
+  }
+  return mc_last_launch();
+}
+
+// kinds 11-15: gin = n input floats in global memory, gout = n output floats
+extern "C" int mc_lab_chain_g(const float *init, float *out, long long *cyc, int n, int reps, int kind,
+                              const float *gin, float *gout, mc_stream_t stream) {
+  if (n <= 0 || n > 8192 || n % 128 || (n & (n - 1)) || reps <= 0) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  switch (kind) {
+    case 11: k_lab_chain_sgpr<11><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 12: k_lab_chain_sgpr<12><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 13: k_lab_chain_sgpr<13><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 14: k_lab_chain_sgpr<14><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 15: k_lab_chain_sgpr<15><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 16: k_lab_chain_sgpr<13, 4><<<1, 256, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 17: k_lab_chain_sgpr<13, 2><<<1, 128, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 18: k_lab_chain_sgpr<13, 8><<<1, 512, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 19: k_lab_chain_sgpr<19><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 20: k_lab_chain_sgpr<20><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 21: k_lab_chain_sgpr<21><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 22: k_lab_chain_sgpr<22><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 23: k_lab_chain_sgpr<23><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 25: k_lab_chain_sgpr<25><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();

@@ -9,13 +9,22 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from lab.lablib import lab as _lab  # noqa: E402
 
-NAMES = {0: "register-only", 1: "product (fsw_chain)", 2: "strict interleave", 3: "reads only", 4: "DPP-fed adds"}
+NAMES = {0: "register-only", 1: "product (fsw_chain)", 2: "strict interleave", 3: "reads only", 4: "DPP-fed adds",
+         5: "rot G16 NS4", 6: "rot G16 NS8", 7: "rot G32 NS4", 8: "rot G16 NS4 ld-first", 9: "rot G8 NS8",
+         10: "rot G16 NS8 ld-first", 11: "SGPR-fed, no stores", 12: "SGPR-fed, LDS stores",
+         13: "SGPR-fed, global stores", 14: "LDS-fed, global stores", 15: "SGPR-fed, lane-gathered stores",
+         16: "SGPR-fed x4 waves, split stores", 17: "SGPR-fed x2 waves, split stores",
+         18: "SGPR-fed x8 waves, split stores", 19: "SGPR-fed, every 16th group stored",
+         20: "SGPR-fed, 4-B global stores", 21: "SGPR-fed, stores one group late",
+         22: "SGPR-fed, all-lane stores one group late", 23: "SGPR-fed, all-lane stores",
+         24: "LDS-fed all lanes, LDS stores", 25: "LDS-fed all lanes, global stores"}
 
 
 def main():
@@ -26,13 +35,32 @@ def main():
     out = torch.empty(4, device=dev)
     cyc = torch.zeros(2, dtype=torch.int64, device=dev)
     n, reps = 8192, 64
+    gin = torch.randn(n, device=dev)
+    gout = torch.zeros(n, device=dev)
+
+    def run(kind, r=reps):
+        if kind < 11 or kind == 24:
+            return lab.mc_lab_chain(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, r, kind, st)
+        return lab.mc_lab_chain_g(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, r, kind, gin.data_ptr(),
+                                  gout.data_ptr(), st)
+
+    # the global-output kinds must write numpy's float32 cumsum of gin
+    bad = []
+    want = np.cumsum(gin.cpu().numpy())
+    for kind in (13, 15, 16, 17, 18, 20, 21, 22, 23):
+        gout.zero_()
+        assert run(kind, 1) == 0
+        torch.cuda.synchronize()
+        if not np.array_equal(gout.cpu().numpy().view(np.uint32), want.view(np.uint32)):
+            bad.append(kind)
+    print("chain correctness failures:", bad, flush=True)
     rows = []
     for rnd in range(3):
         for kind in NAMES:
-            assert lab.mc_lab_chain(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, reps, kind, st) == 0
+            assert run(kind) == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            assert lab.mc_lab_chain(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, reps, kind, st) == 0
+            assert run(kind) == 0
             e1.record()
             e1.synchronize()
             t = e0.elapsed_time(e1) * 1e-3
