@@ -327,10 +327,12 @@ MC_DEV mc_u32x4 delta_vec(mc_u32x4 x, uint32_t p_lo, uint32_t p_hi) {
 // SW: bit 0 = the input is big-endian, bit 1 = the output is (the bytes of
 // each element reversed after the load / before the store, v_perm_b32).
 // FL: f4 / f8 (float differences; the first element is copied as it is).
-template <int ES, int SW = 0, bool FL = false>
+// NV: 16-B vectors per thread (mc_sched.delta_enc_dv: DE_V or 2 x DE_V)
+template <int ES, int SW = 0, bool FL = false, int NV = DE_V>
 __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__restrict__ src,
                                                              uint8_t *__restrict__ dst, size_t nbytes,
                                                              size_t src_stride, size_t dst_stride) {
+  constexpr int DE_V = NV;
   src += (size_t)blockIdx.y * src_stride;  // chunk blockIdx.y of a batch
   dst += (size_t)blockIdx.y * dst_stride;
   const int lane = threadIdx.x & 63;
@@ -352,16 +354,19 @@ __global__ __launch_bounds__(MC_BLOCK) void k_delta_enc_same(const uint8_t *__re
       q_hi[r] = *reinterpret_cast<const uint32_t *>(src + off - 4);
       if (ES == 8) q_lo[r] = *reinterpret_cast<const uint32_t *>(src + off - 8);
     }
+  }
+  // the byte swaps of a big-endian input only after every load is issued: a
+  // swap between them (the lane-0 loads are branches) waited for each load
+  // before the next was issued (7 % slower than little-endian)
+#pragma unroll
+  for (int r = 0; r < DE_V; ++r) {
+    const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
     if constexpr (SW & 1) {  // big-endian input: every element to register order
       x[r] = mc_bswap_vec<ES>(x[r]);
       const mc_u32x4 q = mc_bswap_vec<ES>(mc_u32x4{q_lo[r], q_hi[r], 0u, 0u});
       q_lo[r] = q.x;
       q_hi[r] = q.y;
     }
-  }
-#pragma unroll
-  for (int r = 0; r < DE_V; ++r) {
-    const size_t off = tb + (size_t)r * 16 * MC_BLOCK + 16 * (size_t)threadIdx.x;
     // the previous 8 bytes: lane - 1's last dwords, lane 0's read above
     const uint32_t p_hi = mc_wave_shr1(x[r].w, q_hi[r]), p_lo = mc_wave_shr1(x[r].z, q_lo[r]);
     mc_u32x4 y = delta_vec<ES, FL>(x[r], p_lo, p_hi);
@@ -449,15 +454,23 @@ static McNum num_scalar(int dt, double f, int64_t i) {
   return r;
 }
 
+template <int ES, bool FL, int NV>
+static void launch_delta_same_nv(int sw, dim3 g, const uint8_t *s, uint8_t *d, size_t nbytes, size_t ss, size_t ds,
+                                 hipStream_t st) {
+  g.x = (unsigned)((nbytes + (size_t)NV * 16 * MC_BLOCK - 1) / ((size_t)NV * 16 * MC_BLOCK));
+  switch (sw) {
+    case 0: k_delta_enc_same<ES, 0, FL, NV><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 1: k_delta_enc_same<ES, 1, FL, NV><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    case 2: k_delta_enc_same<ES, 2, FL, NV><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+    default: k_delta_enc_same<ES, 3, FL, NV><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
+  }
+}
+// g.y = the batch rows; g.x follows from nbytes and the vectors per thread
 template <int ES, bool FL = false>
 static void launch_delta_same(int sw, dim3 g, const uint8_t *s, uint8_t *d, size_t nbytes, size_t ss, size_t ds,
                               hipStream_t st) {
-  switch (sw) {
-    case 0: k_delta_enc_same<ES, 0, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    case 1: k_delta_enc_same<ES, 1, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    case 2: k_delta_enc_same<ES, 2, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-    default: k_delta_enc_same<ES, 3, FL><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, ss, ds); break;
-  }
+  if (mc_sched.delta_enc_dv == 2 * DE_V) launch_delta_same_nv<ES, FL, 2 * DE_V>(sw, g, s, d, nbytes, ss, ds, st);
+  else launch_delta_same_nv<ES, FL, DE_V>(sw, g, s, d, nbytes, ss, ds, st);
 }
 
 }  // namespace
@@ -566,7 +579,7 @@ int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t 
     } else if (same && al16 && delta_enc_vec_enabled()) {
       const size_t per = (size_t)DE_V * 16 * MC_BLOCK;
       const dim3 g2((unsigned)((n * ss + per - 1) / per), grid.y);
-      if (same == 1) k_delta_enc_same<1><<<g2, MC_BLOCK, 0, st>>>(sc, dc, n, src_stride, dst_stride);
+      if (same == 1) launch_delta_same<1>(0, g2, sc, dc, n, src_stride, dst_stride, st);
       else if (same == 2) launch_delta_same<2>(sw, g2, sc, dc, n * 2, src_stride, dst_stride, st);
       else if (same == 4) launch_delta_same<4>(sw, g2, sc, dc, n * 4, src_stride, dst_stride, st);
       else launch_delta_same<8>(sw, g2, sc, dc, n * 8, src_stride, dst_stride, st);

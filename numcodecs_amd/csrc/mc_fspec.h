@@ -137,22 +137,26 @@ MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, int a,
     // default-policy loads: the apply pass re-reads what the reduce pass read
     // and finds part of it in the Infinity Cache (256 MiB f4 smooth decode
     // 158-162 -> 154 us against nontemporal loads; f8 unchanged)
+    // every load first, then the byte swaps / conversions: a swap between
+    // the (bounds-branched) loads waited for each load before the next issued
+    typename Tr::svec xs[FS_Q];
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q) {
       const size_t e0 = fs_elem0<D>(t0, q);
       if (e0 + W <= n) {
-        typename Tr::svec x = *reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S));
-        if constexpr ((SW & 1) != 0) x = fs_bswap(x);
-#pragma unroll
-        for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
+        xs[q] = *reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S));
       } else {
 #pragma unroll
-        for (int e = 0; e < W; ++e) {
-          typename Tr::S c = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
-          if constexpr ((SW & 1) != 0) c = fs_bswap_scalar(c);
-          v[q][e] = (typename Tr::V)c;
-        }
+        for (int e = 0; e < W; ++e)
+          xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
       }
+    }
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      typename Tr::svec x = xs[q];
+      if constexpr ((SW & 1) != 0) x = fs_bswap(x);
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
     }
   } else if constexpr (A_ == MC_F4 && D == MC_F8) {
     static_assert((SW & 1) == 0, "big-endian f4 input takes the runtime-astype instance");
@@ -622,25 +626,33 @@ MC_DEV void fsw_load(const uint8_t *src, size_t n, size_t t0, int a,
                      typename FsT<A_, D>::V (&v)[FS_Q][FsT<A_, D>::W]) {
   using Tr = FsT<A_, D>;
   constexpr int W = Tr::W;
+  if constexpr (A_ == D) {  // every load first, then the swaps / conversions (see fs_load)
+    typename Tr::svec xs[FS_Q];
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
+      if (e0 + W <= n) {
+        xs[q] = __builtin_nontemporal_load(
+            reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
+      } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e)
+          xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < FS_Q; ++q) {
+      typename Tr::svec x = xs[q];
+      if constexpr ((SW & 1) != 0) x = fs_bswap(x);
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
     const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
-    if constexpr (A_ == D) {
-      if (e0 + W <= n) {
-        typename Tr::svec x =
-            __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
-        if constexpr ((SW & 1) != 0) x = fs_bswap(x);
-#pragma unroll
-        for (int e = 0; e < W; ++e) v[q][e] = (typename Tr::V)x[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < W; ++e) {
-          typename Tr::S c = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
-          if constexpr ((SW & 1) != 0) c = fs_bswap_scalar(c);
-          v[q][e] = (typename Tr::V)c;
-        }
-      }
-    } else {
+    {
       const int as = mc_itemsize(a);
       uint64_t b[W];
 #pragma unroll

@@ -117,6 +117,18 @@ def check_delta_int():
     return ok
 
 
+def check_delta_same_type():
+    """k_delta_enc_same: every width, both byte orders, integers and floats"""
+    ok = check_delta_int()
+    for dt in ("<f4", ">f4", "<f8", ">i2", ">i8"):
+        d = np.dtype(dt)
+        n = (1 << 22) // d.itemsize + 5
+        x = (rng.standard_normal(n) * 100).astype(d)
+        enc = Delta(dtype=dt).encode(torch.from_numpy(x.view(np.uint8).copy()).to(dev))
+        ok &= _h(enc) == oracle.delta_encode(x, dt).tobytes()
+    return ok
+
+
 def check_delta_float():
     ok = True
     for dt in ("<f4", "<f8"):
@@ -159,6 +171,7 @@ PLAN = {
     "fspec": ([0], check_delta_float),
     "fastdiv": ([0], check_fso),
     "crc_lds": ([1], check_checksums),
+    "delta_enc_dv": ([8], check_delta_same_type),
 }
 
 

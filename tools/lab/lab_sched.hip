@@ -38,6 +38,7 @@ const field kFields[] = {
     {"fspec", "MCODEC_FSPEC", &mc_sched.fspec},
     {"fastdiv", "MCODEC_FASTDIV", &mc_sched.fastdiv},
     {"crc_lds", "MCODEC_CRC_LDS", &mc_sched.crc_lds},
+    {"delta_enc_dv", "MCODEC_DELTA_ENC_DV", &mc_sched.delta_enc_dv},
 };
 
 __attribute__((constructor)) void lab_sched_from_env() {
