@@ -541,19 +541,11 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
     for (; j + 2 * FSW_G <= cnt; j += 2 * FSW_G) {
       ser_ld<T, FSW_G>(p + j + FSW_G, gb);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k = 0; k < FSW_G; ++k) {
-        acc = ser_add<D>(acc, ga[k]);
-        ga[k] = acc;
-      }
+      acc = ser_group<D, FSW_G>(acc, ga);
       ser_st<T, FSW_G>(o + j, ga);
       ser_ld<T, FSW_G>(p + j + 2 * FSW_G, ga);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k = 0; k < FSW_G; ++k) {
-        acc = ser_add<D>(acc, gb[k]);
-        gb[k] = acc;
-      }
+      acc = ser_group<D, FSW_G>(acc, gb);
       ser_st<T, FSW_G>(o + j + FSW_G, gb);
     }
   }

@@ -209,6 +209,46 @@ MC_DEV typename SerAcc<D>::T ser_add(typename SerAcc<D>::T a, typename SerAcc<D>
   }
 }
 
+// One group of the chain, in place (g[k] <- the running sum after g[k]).
+// f2: numpy adds in float32 and rounds to half; with float32's 24 >= 2*11+2
+// bits that double rounding equals one correctly rounded half add, so the
+// group runs as a chain of half adds (v_add_f16, one dependent op per
+// element; LLVM folds the float<->half round trips between them).  NaN is
+// absorbing in the chain, so a group ending in NaN is recomputed with the
+// exact routine (ser_add: numpy's payload-preserving conversion, x86's NaN
+// choice) from its first value -- the GPU's own NaN results differ (inf +
+// -inf is +NaN here, -NaN on x86).
+template <int D, int G>
+MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAcc<D>::T (&g)[G]) {
+  using T = typename SerAcc<D>::T;
+  if constexpr (D == MC_F2) {
+    const T a0 = acc;
+    T r[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      acc = (float)((_Float16)acc + (_Float16)g[k]);
+      r[k] = acc;
+    }
+    if (__builtin_isnan(acc)) {
+      acc = a0;
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        acc = ser_add<D>(acc, g[k]);
+        r[k] = acc;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G; ++k) g[k] = r[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      acc = ser_add<D>(acc, g[k]);
+      g[k] = acc;
+    }
+  }
+  return acc;
+}
+
 // G chain values as 16-B LDS accesses (p 16-B aligned)
 template <typename T, int SER_G>
 MC_DEV void ser_ld(const T *p, T (&r)[SER_G]) {

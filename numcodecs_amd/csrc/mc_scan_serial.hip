@@ -155,19 +155,11 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
         for (; j + 2 * SER_G <= cnt; j += 2 * SER_G) {
           ser_ld<T, SER_G>(p + j + SER_G, gb);
           __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead ahead of the adds
-#pragma unroll
-          for (int k = 0; k < SER_G; ++k) {
-            acc = ser_add<L>(acc, ga[k]);
-            ga[k] = acc;
-          }
+          acc = ser_group<L, SER_G>(acc, ga);
           ser_st<T, SER_G>(o + j, ga);
           ser_ld<T, SER_G>(p + j + 2 * SER_G, ga);
           __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int k = 0; k < SER_G; ++k) {
-            acc = ser_add<L>(acc, gb[k]);
-            gb[k] = acc;
-          }
+          acc = ser_group<L, SER_G>(acc, gb);
           ser_st<T, SER_G>(o + j + SER_G, gb);
         }
       }

@@ -3,7 +3,7 @@
 HIP events on the launch stream; one JSON line.  The first call of each case
 is checked byte for byte against numpy's cumsum (the oracle's expression).
 
-    python tools/probe_fspec_walk.py [f4|f8] [MiB]
+    python tools/probe_fspec_walk.py [f2|f4|f8] [MiB] [quick]   (KINDS=smooth,randn,... to select)
 """
 import json
 import os
@@ -21,7 +21,7 @@ dt = sys.argv[1] if len(sys.argv) > 1 else "f4"
 mib = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 quick = len(sys.argv) > 3 and sys.argv[3] == "quick"  # single chunk only, no batches
 npdt = np.dtype("<" + dt)
-tdt = {"f4": torch.float32, "f8": torch.float64}[dt]
+tdt = {"f2": torch.float16, "f4": torch.float32, "f8": torch.float64}[dt]
 dev = torch.device("cuda", 0)
 codec = Delta("<" + dt)
 
@@ -42,7 +42,8 @@ def timed(fn, reps):
 
 out = {"dtype": dt, "MiB": mib}
 n = mib * (1 << 20) // npdt.itemsize
-for kind in ("smooth", "sin4096", "sin_noise", "randwalk", "chirp", "sparse", "smallamp", "randn"):
+KINDS = os.environ.get("KINDS", "smooth,sin4096,sin_noise,randwalk,chirp,sparse,smallamp,randn").split(",")
+for kind in KINDS:
     t0 = time.time()
     x = family(kind, n).astype(npdt)
     enc_h = np.empty_like(x)
