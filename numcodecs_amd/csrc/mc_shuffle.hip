@@ -665,7 +665,7 @@ static int default_variant(size_t es, bool enc, size_t total_bytes, size_t count
   switch (es) {
     case 2: return V_REG | tile_flag(count, 4096, V_BIG4);  // 6.34 / 6.22 TB/s
     // encode: 32768-element tiles (128 KiB per workgroup, 32 16-B loads in
-    // flight per thread): 87.5 against 93.0 us for 64 KiB tiles, 256 MiB
+    // flight per thread): 87.4 against 88.9 us for 64 KiB tiles, 256 MiB
     // (round 4, profiles/r04/probe_shuffle_tiles.json); decode: lane pairs,
     // 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
     // profiles/r01/shuffle4_pair_ab.log; larger pair tiles measured slower)

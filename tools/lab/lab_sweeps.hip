@@ -42,11 +42,19 @@ int mc_lab_c4_dec1p(const void *src, void *dst, size_t n, int astype, int dtype,
 // bits 0-2 layout (0 default, 1 register/dword stores, 2 LDS-staged 16-B
 // stores, 3 LDS both sides, 4 generic byte kernel, 5 lane pairs), | 8
 // temporal accesses, | 16 / | 128 2x / 4x tiles, bits 5-6 tile group,
-// | 256 software-pipelined persistent loop, | 512 8x tiles; max_blocks 0 =
-// default grid.
+// | 256 software-pipelined persistent loop, | 512 8x tiles.  max_blocks 0 =
+// one workgroup per tile, the product's grid for large buffers (round 4:
+// until then 0 capped an explicit layout at MC_MAX_GRID = 2048 workgroups,
+// which made every layout with more than 2048 tiles loop and measure slower
+// than it runs in the product); < 0 = that 2048 cap; > 0 = this cap.
+static int lab_grid_cap(int max_blocks) {
+  return max_blocks == 0 ? 0x7fffffff : max_blocks < 0 ? (int)MC_MAX_GRID : max_blocks;
+}
+
 int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize, int encode,
                            int variant, int max_blocks, mc_stream_t stream) {
   if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  max_blocks = lab_grid_cap(max_blocks);
   return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
                          (hipStream_t)stream);
 }
@@ -60,6 +68,7 @@ int mc_lab_bitround_shuffle_variant(const void *src, void *dst, size_t n, int it
   const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
   if (keepbits < 0 || keepbits >= mbits) return MC_EINVAL;
   const McBitRound br = mc_make_bitround(itemsize, keepbits);
+  max_blocks = lab_grid_cap(max_blocks);
   return mc_shuffle_impl(src, 0, dst, 0, 1, n * (size_t)itemsize, (size_t)itemsize, true, variant, max_blocks, &br,
                          (hipStream_t)stream);
 }

@@ -1,5 +1,7 @@
 """Shuffle tile-size sweep (round 4): the product layouts with 1x..8x tiles
-(mc_shuffle.hip V_BIG / V_BIG4 / V_BIG8) for es = 2, 4, 8, encode and
+(mc_shuffle.hip V_BIG / V_BIG4 / V_BIG8), one workgroup per tile as the
+product launches them (lab max_blocks 0; before round 4's fix that meant a
+2048-workgroup cap), for es = 2, 4, 8, encode and
 decode, the BitRound-fused encode, the lab encodes of lab_shuffle4.hip and
 the copy calibration -- interleaved rounds, 4 rotating 256 MiB buffer sets.
 
