@@ -26,7 +26,7 @@ from . import _native, _ops
 from ._native import check, lib
 from .bitround import BitRound, max_bits
 from .compat import device_out_bytes, ensure_contiguous_ndarray, is_device_tensor
-from .delta import Delta, check_decode_pair, check_first_elements
+from .delta import Delta, check_first_elements, decode_loop_dtype
 from .fixedscaleoffset import FixedScaleOffset, _resolve
 from .fletcher32 import Fletcher32, _mismatch
 from .shuffle import Shuffle
@@ -112,10 +112,18 @@ def delta_chunks(chunks, delta, encode=True, out=None):
         raise IndexError("index 0 is out of bounds for axis 0 with size 0")
     if encode and b:
         check_first_elements(rows[:, : src_t.itemsize], delta.dtype, delta.astype)
-    if not encode:
-        check_decode_pair(delta.astype, delta.dtype)
+    loop = None if encode else decode_loop_dtype(delta.astype, delta.dtype)
     m = n * dst_t.itemsize
     out = torch.empty((b, m), dtype=torch.uint8, device=rows.device) if out is None else _as_rows(out)
+    if loop is not None:
+        # a pair decoded through its loop dtype (delta.decode_loop_dtype):
+        # the running sums of every row in `loop`, then one cast of them all
+        if b and n:
+            sums = delta_chunks(rows, Delta(dtype=loop, astype=delta.astype), encode=False)
+            cast = torch.empty((b, m), dtype=torch.uint8, device=rows.device)
+            _ops.cast(sums, cast, b * n, loop, delta.dtype)
+            out.copy_(cast)
+        return out
     if not encode and b and nb >= _LARGE_ROW and rows.data_ptr() % 16 == 0 and \
             rows.stride(0) % 16 == 0 and out.stride(0) % 16 == 0 and out.data_ptr() % 16 == 0:
         # huge rows: each decoded by the whole chip (mc_delta_decode), not by

@@ -8,6 +8,7 @@ numpy's exact left-to-right order for float dtypes.
 """
 
 import numpy as np
+import torch
 
 from . import _ops
 from .abc import Codec
@@ -30,21 +31,31 @@ def check_first_elements(firsts, dtype, astype) -> None:
         tmp[0] = v
 
 
-def check_decode_pair(astype, dtype) -> None:
+def decode_loop_dtype(astype, dtype):
     """np.cumsum(enc, out=dec) (delta.py:80) accepts every numeric pair: it
-    accumulates in np.promote_types(astype, dtype) and casts each running sum
-    to dtype.  The device decode reproduces that for a float dtype (any
-    astype) and for an integer dtype with an integer/bool astype (wrap-around
-    sums: accumulating in the wider integer and casting back is the same
-    modulo 2^bits) and bool from bool (logical or).  A float astype into an
-    integer/bool dtype (a float running sum, truncated per element) and an
-    integer astype into bool (a nonzero test of an integer running sum) are
-    not implemented and raise instead of returning different bytes."""
+    accumulates in np.promote_types(astype, dtype) and casts each running
+    sum to dtype.  The device decode computes that directly for a float
+    dtype (any astype), an integer dtype from an integer/bool astype
+    (wrap-around sums: accumulating in the wider integer and casting back is
+    the same modulo 2^bits) and bool from bool (logical or); it returns None
+    for those.  For the other two families -- a float astype into an
+    integer/bool dtype (a float running sum, cast per element) and an
+    integer astype into bool (a nonzero test of an integer running sum) --
+    it returns the loop dtype L: the decode runs as Delta(L, astype) (a
+    supported pair, the running sums exactly as numpy keeps them) followed
+    by numpy's cast L -> dtype (mc_cast)."""
     a, d = np.dtype(astype), np.dtype(dtype)
     if d.kind in "iub" and a.kind == "f" or d.kind == "b" and a.kind != "b":
-        raise NotImplementedError(
-            f"Delta decode of {a.str!r} into {d.str!r} (a running sum in "
-            f"{np.promote_types(a, d).str!r} cast to {d.str!r}) is not implemented on the device")
+        return np.promote_types(a, d)
+    return None
+
+
+def decode_two_step(src, dst, n, astype, dtype, loop) -> None:
+    """Delta decode of a pair decode_loop_dtype() routes through its loop
+    dtype: running sums into a device temporary of `loop`, then cast."""
+    tmp = torch.empty(n * loop.itemsize, dtype=torch.uint8, device=src.device)
+    _ops.delta_decode(src, tmp, n, astype, loop)
+    _ops.cast(tmp, dst, n, loop, dtype)
 
 
 class Delta(Codec):
@@ -86,10 +97,13 @@ class Delta(Codec):
         if src.nbytes % self.astype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.astype.itemsize
-        check_decode_pair(self.astype, self.dtype)
+        loop = decode_loop_dtype(self.astype, self.dtype)
         direct = device_out_bytes(out, n * self.dtype.itemsize, src)
         dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
-        _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)
+        if loop is None:
+            _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)
+        elif n:
+            decode_two_step(src.data, dst, n, self.astype, self.dtype, loop)
         if direct is not None:
             return out
         return ndarray_copy(finish(dst, self.dtype, (n,), "C", src.host), out)

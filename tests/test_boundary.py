@@ -228,19 +228,19 @@ def test_is_ndarray_like_mirrors_reference_protocol():
 
 def test_delta_decode_pairs():
     """np.cumsum(enc, out=dec) (delta.py:80) accepts every numeric pair (it
-    accumulates in promote_types(astype, dtype)); the device covers float
-    dtypes, integer-from-integer (wrap-around) and bool-from-bool, and
-    refuses the two families whose running sum it does not reproduce."""
+    accumulates in promote_types(astype, dtype)); the device decodes float
+    dtypes, integer-from-integer (wrap-around) and bool-from-bool directly,
+    and the two other families through their loop dtype and a cast."""
     import itertools
 
-    from numcodecs_amd.delta import check_decode_pair
+    from numcodecs_amd.delta import decode_loop_dtype
 
     ts = ["|b1", "|i1", "<i2", ">i4", "<i8", "|u1", ">u2", "<u4", "<u8", "<f2", ">f4", "<f8"]
     for a, d in itertools.product(ts, ts):
         ka, kd = np.dtype(a).kind, np.dtype(d).kind
-        refused = (kd in "iub" and ka == "f") or (kd == "b" and ka != "b")
-        if refused:
-            with pytest.raises(NotImplementedError):
-                check_decode_pair(a, d)
+        two_step = (kd in "iub" and ka == "f") or (kd == "b" and ka != "b")
+        loop = decode_loop_dtype(a, d)
+        if two_step:
+            assert loop == np.promote_types(a, d) and loop.isnative, (a, d)
         else:
-            check_decode_pair(a, d)
+            assert loop is None, (a, d)

@@ -278,3 +278,43 @@ def test_float_delta_decode_nan_payloads(device, dt, n):
     y[-1] = -np.inf
     dec = Delta(dt).decode(torch.from_numpy(y.view(np.uint8).copy()).to(device))
     assert dec.contiguous().view(torch.uint8).cpu().numpy().tobytes() == _oracle_dec(y, dt, dt).tobytes()
+
+
+TWO_STEP_PAIRS = [("<i4", "<f4"), ("<i2", "<f8"), ("|b1", "<f4"), ("|u1", "<f2"), ("<i8", "<f8"), (">i4", ">f4"),
+                  ("<u2", "<f4"), ("|b1", "<i4"), ("|b1", "|u1"), ("|b1", ">i2"), ("|i1", "<f2")]
+
+
+def _two_step_input(astype, n, seed):
+    rng = np.random.default_rng(seed)
+    a = np.dtype(astype)
+    if a.kind == "f":
+        x = (rng.standard_normal(n) * 2.5).astype(a)
+        if n > 40:
+            x[n // 4] = np.nan if n % 2 else np.inf
+            x[n // 3] = -np.inf
+        return x
+    info = np.iinfo(a)
+    return rng.integers(max(info.min, -3), min(info.max, 3), n, endpoint=True).astype(a)
+
+
+@pytest.mark.parametrize("dt,astype", TWO_STEP_PAIRS)
+@pytest.mark.parametrize("n", [1, 5, 4097, 70001])
+def test_delta_decode_through_loop_dtype(device, dt, astype, n):
+    """The pairs decoded through their loop dtype (np.promote_types(astype,
+    dtype)) and a cast -- a float running sum into integers or bools, an
+    integer running sum into bools -- byte-identical to np.cumsum(enc,
+    out=dec) (delta.py:80), single chunk and batched rows."""
+    enc = _two_step_input(astype, n, n)
+    ref = _oracle_dec(enc, dt, astype)
+    codec = Delta(dt, astype)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        got = codec.decode(torch.from_numpy(enc.view(np.uint8).copy()).to(device))
+    assert got.contiguous().view(torch.uint8).cpu().numpy().tobytes() == ref.tobytes(), (dt, astype, n)
+    if n < 70001:
+        b = 5
+        rows = np.stack([_two_step_input(astype, n, n + k) for k in range(b)])
+        dec = batch.delta_chunks(torch.from_numpy(rows.view(np.uint8).reshape(b, -1).copy()).to(device), codec,
+                                 encode=False).cpu().numpy()
+        for k in range(b):
+            assert dec[k].tobytes() == _oracle_dec(rows[k], dt, astype).tobytes(), (dt, astype, n, k)
