@@ -607,17 +607,22 @@ def copy_ceiling(dev, nbytes: int = GiB, reps: int = 10) -> dict:
     a.fill_(1)
     st = torch.cuda.current_stream(dev).cuda_stream
 
-    def rate(fn, nb, sets=1):
+    def rate(fn, nb, sets=1, groups=3):
+        # back-to-back launches between one event pair, as the headline's
+        # mean_launch_ms is measured (round 4: one launch per event pair
+        # added the launch ramp and drain to every sample, ~3-5 % of an
+        # 85 us copy, and put the ceiling below the kernels it bounds)
         for i in range(sets):
             fn(i)
         ts = []
-        for r in range(reps):
+        for _ in range(groups):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            fn(r % sets)
+            for r in range(reps):
+                fn(r % sets)
             e1.record()
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e-3)
+            ts.append(e0.elapsed_time(e1) * 1e-3 / reps)
         ts.sort()
         return round(2 * nb / ts[len(ts) // 2] / 1e9, 1)
 

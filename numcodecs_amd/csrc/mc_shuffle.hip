@@ -659,17 +659,23 @@ static int tile_flag(size_t count, size_t base_elems, int want) {
   return 0;
 }
 
-static int default_variant(size_t es, bool enc, size_t total_bytes, size_t count, unsigned *grid_cap) {
+static int default_variant(size_t es, bool enc, size_t total_bytes, size_t count, size_t nchunks,
+                           unsigned *grid_cap) {
   *grid_cap = 0x7fffffffu;
   if (total_bytes < ((size_t)64 << 20)) return V_REG;
   switch (es) {
     case 2: return V_REG | tile_flag(count, 4096, V_BIG4);  // 6.34 / 6.22 TB/s
-    // encode: 32768-element tiles (128 KiB per workgroup, 32 16-B loads in
-    // flight per thread): 87.4 against 88.9 us for 64 KiB tiles, 256 MiB
-    // (round 4, profiles/r04/probe_shuffle_tiles.json); decode: lane pairs,
-    // 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
+    // encode of one chunk: 32768-element tiles (128 KiB per workgroup, 32
+    // 16-B loads in flight per thread): 87.4 against 88.9 us for 64 KiB
+    // tiles, 256 MiB (round 4, profiles/r04/probe_shuffle_tiles.json); a
+    // batch of chunks under 64 MiB: lane pairs on 2x tiles, 256 x 1 MiB
+    // 98.3 -> 85.5 us, 64 x 4 MiB 93.2 -> 85.0 us (the 128 KiB tiles lose
+    // 6-13 % there, profiles/r04/probe_batch_variants.json); decode: lane
+    // pairs, 8-B plane loads (5.96 vs 5.81 TB/s interleaved,
     // profiles/r01/shuffle4_pair_ab.log; larger pair tiles measured slower)
-    case 4: return enc ? (V_REG | tile_flag(count, 4096, V_BIG8)) : (V_PAIR | tile_flag(count, 4096, V_BIG));
+    case 4:
+      if (enc && nchunks > 1 && count * 4 < ((size_t)64 << 20)) return V_PAIR | tile_flag(count, 4096, V_BIG);
+      return enc ? (V_REG | tile_flag(count, 4096, V_BIG8)) : (V_PAIR | tile_flag(count, 4096, V_BIG));
     case 8:  // lane pairs keep the 8-B element side lane-contiguous
       return enc ? V_PAIR : (V_PAIR | tile_flag(count, 2048, V_BIG));  // 5.89 / 6.11 TB/s
     default:
@@ -846,7 +852,7 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
 
   unsigned default_cap = MC_MAX_GRID;
   if (variant == V_DEFAULT) {
-    variant = default_variant(es, enc, chunk_bytes * nchunks, m.count, &default_cap);
+    variant = default_variant(es, enc, chunk_bytes * nchunks, m.count, nchunks, &default_cap);
     if (max_blocks <= 0) max_blocks = (int)default_cap;
   }
   const bool fast_es = es == 2 || es == 4 || es == 8 || es == 16;

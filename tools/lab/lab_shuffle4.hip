@@ -25,6 +25,10 @@
 //   kind 9  as 4 with default-policy LDS-DMA loads
 //   kind 10 as 8 with the quad-major store order
 //   kind 11 register staging, Q = 64 (four tiles' loads in flight)
+//   kinds 12-15  kind 8 (Q = 32, the product's tile) with the tiles spread:
+//           workgroup b takes tile (b % S) * ntiles/S + b / S, so the
+//           workgroups in flight write S far-apart regions of every plane
+//           instead of one (S = 2, 4, 16, 64)
 #include "mc_shuffle.h"
 
 namespace {
@@ -32,14 +36,14 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
-MC_DEV size_t lab_tile(bool xcd, size_t ntiles) {
+MC_DEV size_t lab_tile(int spread, size_t ntiles) {
   const size_t b = blockIdx.x;
-  if (!xcd) return b;
-  const size_t per = ntiles / 8;  // the host checks ntiles % 8 == 0
-  return (b % 8) * per + b / 8;
+  if (spread <= 1) return b;
+  const size_t per = ntiles / spread;  // the host checks ntiles % spread == 0
+  return (b % spread) * per + b / spread;
 }
 
-template <int Q, int ORDER, bool XCD, bool PERM>
+template <int Q, int ORDER, int XCD, bool PERM>
 __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                           size_t count, size_t ntiles) {
   constexpr size_t TE = (size_t)Q * 4 * MC_BLOCK;
@@ -70,7 +74,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__rest
   }
 }
 
-template <int Q, bool XCD, int AUX>
+template <int Q, int XCD, int AUX>
 __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_glds(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                            size_t count, size_t ntiles) {
   constexpr size_t TE = (size_t)Q * 4 * MC_BLOCK;
@@ -141,27 +145,32 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_quadlane(const uint8_t *_
 
 extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, int kind, mc_stream_t stream) {
   hipStream_t st = (hipStream_t)stream;
-  const int Q = (kind == 4 || kind == 9) ? 8 : (kind == 8 || kind == 10) ? 32 : kind == 11 ? 64 : 16;
+  const int Q = (kind == 4 || kind == 9) ? 8 : (kind == 8 || kind == 10 || kind >= 12) ? 32 : kind == 11 ? 64 : 16;
   const size_t tb = (size_t)Q * 4 * MC_BLOCK * 4;  // tile bytes
   if (!src || !dst || nbytes == 0 || nbytes % tb || (uintptr_t)src % 16 || (uintptr_t)dst % 16) return MC_EINVAL;
   const size_t count = nbytes / 4, ntiles = nbytes / tb;
   if ((kind == 2 || kind == 5) && ntiles % 8) return MC_EINVAL;
+  if (kind >= 12 && ntiles % 64) return MC_EINVAL;
   const unsigned g = (unsigned)ntiles;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
   switch (kind) {
-    case 0: k_lab_enc4_reg<16, 0, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 1: k_lab_enc4_reg<16, 1, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 2: k_lab_enc4_reg<16, 0, true, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 3: k_lab_enc4_glds<16, false, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 4: k_lab_enc4_glds<8, false, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 5: k_lab_enc4_glds<16, true, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 9: k_lab_enc4_glds<8, false, 0><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 0: k_lab_enc4_reg<16, 0, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 1: k_lab_enc4_reg<16, 1, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 2: k_lab_enc4_reg<16, 0, 8, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 3: k_lab_enc4_glds<16, 0, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 4: k_lab_enc4_glds<8, 0, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 5: k_lab_enc4_glds<16, 8, 2><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 9: k_lab_enc4_glds<8, 0, 0><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 6: k_lab_enc4_quadlane<16><<<g, MC_BLOCK, 0, st>>>(s, d, count); break;
-    case 7: k_lab_enc4_reg<16, 0, false, false><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 8: k_lab_enc4_reg<32, 0, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 10: k_lab_enc4_reg<32, 1, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
-    case 11: k_lab_enc4_reg<64, 0, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 7: k_lab_enc4_reg<16, 0, 0, false><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 8: k_lab_enc4_reg<32, 0, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 10: k_lab_enc4_reg<32, 1, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 11: k_lab_enc4_reg<64, 0, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 12: k_lab_enc4_reg<32, 0, 2, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 13: k_lab_enc4_reg<32, 0, 4, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 14: k_lab_enc4_reg<32, 0, 16, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 15: k_lab_enc4_reg<32, 0, 64, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();

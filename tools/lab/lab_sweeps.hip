@@ -59,6 +59,16 @@ int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t ele
                          (hipStream_t)stream);
 }
 
+// a batch of nchunks rows (row strides ss / ds bytes) with an explicit
+// layout, as mc_lab_shuffle_variant
+int mc_lab_shuffle_batch_variant(const void *src, size_t ss, void *dst, size_t ds, size_t nchunks, size_t nbytes,
+                                 size_t elementsize, int encode, int variant, int max_blocks, mc_stream_t stream) {
+  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  max_blocks = lab_grid_cap(max_blocks);
+  return mc_shuffle_impl(src, ss, dst, ds, nchunks, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
+                         (hipStream_t)stream);
+}
+
 // BitRound fused into the Shuffle encode (mc_bitround_shuffle) with an
 // explicit layout, as mc_lab_shuffle_variant.
 int mc_lab_bitround_shuffle_variant(const void *src, void *dst, size_t n, int itemsize, int keepbits,

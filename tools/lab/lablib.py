@@ -15,6 +15,7 @@ LAB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 _V, _S, _I, _D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
 _SIGS = {
     "mc_lab_shuffle_variant": ([_V, _V, _S, _S, _I, _I, _I, _V], _I),
+    "mc_lab_shuffle_batch_variant": ([_V, _S, _V, _S, _S, _S, _S, _I, _I, _I, _V], _I),
     "mc_lab_delta_decode_batch_variant": ([_V, _S, _V, _S, _S, _S, _I, _I, _I, _V], _I),
     "mc_lab_c4_decode_workspace": ([_S], _S),
     "mc_lab_c4_decode_variant": ([_V, _V, _S, _I, _I, _D, _D, _V, _S, _I, _V], _I),
