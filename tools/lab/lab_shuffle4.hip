@@ -29,7 +29,13 @@
 //           workgroup b takes tile (b % S) * ntiles/S + b / S, so the
 //           workgroups in flight write S far-apart regions of every plane
 //           instead of one (S = 2, 4, 16, 64)
+//   kind 16  kind 8 with the plane store order rotated per workgroup
+//           (workgroup b stores planes b, b+1, b+2, b+3 mod 4), so the
+//           workgroups in flight spread their stores over all 4 planes
+//   kind 17  as 16, quad-major order with the rotation
 #include "mc_shuffle.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -61,7 +67,34 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__rest
 #pragma unroll
       for (int b = 0; b < 4; ++b) p[q][b] = w[q][b];
   }
-  if constexpr (ORDER == 0) {
+  if constexpr (ORDER == 2 || ORDER == 3) {
+    auto rot = [&](auto R) {
+      constexpr int r = decltype(R)::value;
+      if constexpr (ORDER == 2) {
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            const int b = (bb + r) & 3;
+            mc_st4<true>(d + (size_t)b * count + (size_t)(q * MC_BLOCK + tid) * 4, p[q][b]);
+          }
+      } else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) {
+            const int b = (bb + r) & 3;
+            mc_st4<true>(d + (size_t)b * count + (size_t)(q * MC_BLOCK + tid) * 4, p[q][b]);
+          }
+      }
+    };
+    switch (blockIdx.x & 3) {
+      case 0: rot(std::integral_constant<int, 0>{}); break;
+      case 1: rot(std::integral_constant<int, 1>{}); break;
+      case 2: rot(std::integral_constant<int, 2>{}); break;
+      default: rot(std::integral_constant<int, 3>{}); break;
+    }
+  } else if constexpr (ORDER == 0) {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -150,7 +183,7 @@ extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, in
   if (!src || !dst || nbytes == 0 || nbytes % tb || (uintptr_t)src % 16 || (uintptr_t)dst % 16) return MC_EINVAL;
   const size_t count = nbytes / 4, ntiles = nbytes / tb;
   if ((kind == 2 || kind == 5) && ntiles % 8) return MC_EINVAL;
-  if (kind >= 12 && ntiles % 64) return MC_EINVAL;
+  if (kind >= 12 && kind <= 15 && ntiles % 64) return MC_EINVAL;
   const unsigned g = (unsigned)ntiles;
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *d = static_cast<uint8_t *>(dst);
@@ -171,6 +204,8 @@ extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, in
     case 13: k_lab_enc4_reg<32, 0, 4, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 14: k_lab_enc4_reg<32, 0, 16, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 15: k_lab_enc4_reg<32, 0, 64, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 16: k_lab_enc4_reg<32, 2, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 17: k_lab_enc4_reg<32, 3, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();
