@@ -1117,7 +1117,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
 // all totals before its range itself (coalesced, 8 loads in flight per
 // thread) and scans its own 256.  A one-workgroup scan (LDS-staged, 4096
 // totals per round) was bound by a single CU's bandwidth: 14.7 us for
-// 16 Ki tiles against 7.9 us here; reading the earlier totals redundantly
+// 16 Ki tiles against 7.9 us here (6.6 us since round 4, 32 loads in flight
+// per thread instead of 8); reading the earlier totals redundantly
 // spreads that over ntiles/256 CUs.  Any association is
 // fine: the apply pass only relies on the stored pre[] and sums[].
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict__ sums,
@@ -1127,14 +1128,27 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict
   __shared__ double lds[2][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t b = (size_t)blockIdx.x * MC_BLOCK;
-  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  size_t i = threadIdx.x;
-  for (; i + 7 * MC_BLOCK < b; i += 8 * MC_BLOCK) {
+  // 32 loads in flight per thread per round trip (8 took ~8 round trips
+  // for the last workgroup of 16 Ki tiles: 8.2 us for the whole kernel)
+  constexpr int PU = 32;
+  double a[PU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] += sums[i + (size_t)k * MC_BLOCK];
+  for (int k = 0; k < PU; ++k) a[k] = 0.0;
+  for (size_t i = threadIdx.x; i < b; i += PU * MC_BLOCK) {
+    double v[PU];  // branch-free: every load issued before the adds
+#pragma unroll
+    for (int k = 0; k < PU; ++k) {
+      const size_t j = i + (size_t)k * MC_BLOCK;
+      v[k] = sums[j < b ? j : b - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < PU; ++k) a[k] += i + (size_t)k * MC_BLOCK < b ? v[k] : 0.0;
   }
-  for (; i < b; i += MC_BLOCK) a[0] += sums[i];
-  double acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int h = PU / 2; h > 0; h >>= 1)
+#pragma unroll
+    for (int k = 0; k < h; ++k) a[k] += a[k + h];
+  double acc = a[0];
   const double x = b + threadIdx.x < ntiles ? sums[b + threadIdx.x] : 0.0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
