@@ -33,6 +33,10 @@
 //           (workgroup b stores planes b, b+1, b+2, b+3 mod 4), so the
 //           workgroups in flight spread their stores over all 4 planes
 //   kind 17  as 16, quad-major order with the rotation
+//   kind 18  kind 8 with default-policy (temporal) plane stores and
+//           nontemporal loads: the Infinity Cache takes the 4 plane streams
+//           and writes them back in its own order
+//   kind 19  kind 8 with default-policy loads and nontemporal stores
 #include "mc_shuffle.h"
 
 #include <type_traits>
@@ -49,7 +53,7 @@ MC_DEV size_t lab_tile(int spread, size_t ntiles) {
   return (b % spread) * per + b / spread;
 }
 
-template <int Q, int ORDER, int XCD, bool PERM>
+template <int Q, int ORDER, int XCD, bool PERM, bool LDNT = true, bool STNT = true>
 __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                           size_t count, size_t ntiles) {
   constexpr size_t TE = (size_t)Q * 4 * MC_BLOCK;
@@ -59,7 +63,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__rest
   uint8_t *d = dst + tile * TE;
   uint32_t w[Q][4], p[Q][4];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) load_quad<4, true>(s + (size_t)(q * MC_BLOCK + tid) * 16, w[q]);
+  for (int q = 0; q < Q; ++q) load_quad<4, LDNT>(s + (size_t)(q * MC_BLOCK + tid) * 16, w[q]);
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     if constexpr (PERM) mc_quad_to_planes<4>(w[q], p[q]);
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_lab_enc4_reg(const uint8_t *__rest
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-      for (int q = 0; q < Q; ++q) mc_st4<true>(d + (size_t)b * count + (size_t)(q * MC_BLOCK + tid) * 4, p[q][b]);
+      for (int q = 0; q < Q; ++q) mc_st4<STNT>(d + (size_t)b * count + (size_t)(q * MC_BLOCK + tid) * 4, p[q][b]);
   } else {
 #pragma unroll
     for (int q = 0; q < Q; ++q)
@@ -206,6 +210,8 @@ extern "C" int mc_lab_shuffle4_enc(const void *src, void *dst, size_t nbytes, in
     case 15: k_lab_enc4_reg<32, 0, 64, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 16: k_lab_enc4_reg<32, 2, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     case 17: k_lab_enc4_reg<32, 3, 0, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 18: k_lab_enc4_reg<32, 0, 0, true, true, false><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
+    case 19: k_lab_enc4_reg<32, 0, 0, true, false, true><<<g, MC_BLOCK, 0, st>>>(s, d, count, ntiles); break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();
