@@ -88,15 +88,35 @@ __all__ = [
 ]
 
 
+def _register_virtual_subclass():
+    """Make every numcodecs_amd codec an instance of ``numcodecs.abc.Codec``
+    (reference: src/numcodecs/abc.py:33, an ``ABC``) by registering our base
+    class as a virtual subclass, so callers that type-check their filters
+    (Zarr's numcodecs wrappers, zarr3.py:16-31) accept these codecs.  Returns
+    True when numcodecs' ABC was found."""
+    try:
+        from numcodecs.abc import Codec as _NcCodec
+    except Exception:
+        return False
+    if not issubclass(Codec, _NcCodec):
+        _NcCodec.register(Codec)
+    return True
+
+
+_register_virtual_subclass()
+
+
 def register_with_numcodecs():
     """Register these classes into an installed ``numcodecs`` registry
-    (replacing the CPU implementations under the same ids).  Returns the
-    list of ids registered, or [] when numcodecs is not importable."""
+    (replacing the CPU implementations under the same ids), and make them
+    virtual subclasses of ``numcodecs.abc.Codec``.  Returns the list of ids
+    registered, or [] when numcodecs is not importable."""
     try:
         import numcodecs  # noqa: F401
         from numcodecs.registry import register_codec as _nc_register
     except Exception:
         return []
+    _register_virtual_subclass()
     ids = []
     for cls in (Delta, Quantize, FixedScaleOffset, Shuffle, BitRound, Fletcher32, CRC32, CRC32C,
                 Adler32, JenkinsLookup3, AsType, PackBits):

@@ -5,8 +5,9 @@ CRC32, CRC32C, Adler32 and JenkinsLookup3 with the reference's framing:
 payload (``location='start'``) or the payload followed by it (``'end'``), and
 ``decode`` verifies it and returns the payload, raising the reference's
 RuntimeError on a mismatch.  The checksums run on the GPU
-(csrc/mc_checksum.hip): CRC32/CRC32C as table-driven slicing-by-16 with GF(2)
-tile combination, Adler32 as a weighted parallel reduction, Jenkins lookup3
+(csrc/mc_checksum.hip, mc_crc_bs.hip): CRC32/CRC32C as a generated bit-sliced
+XOR network over each loaded dword (no table lookups, since round 3) with
+GF(2) tile combination, Adler32 as a weighted parallel reduction, Jenkins lookup3
 serially per chunk (its mixing rounds have no parallel form; batches of chunks
 run in parallel, see ``numcodecs_amd.batch.checksum32_chunks``).
 
