@@ -98,7 +98,7 @@ def visible_gpu_count() -> "tuple[int, str]":
     return n, "/sys/class/kfd/kfd/topology"
 
 
-def launch_ranks(n: int, dry_run: bool) -> int:
+def launch_ranks(n: int, dry_run: bool, extra_env: "dict | None" = None) -> int:
     """Start n rank processes of this script (one per GPU) and wait for them.
 
     Runs in the parent, which never touches the GPU: devices are counted from
@@ -116,7 +116,7 @@ def launch_ranks(n: int, dry_run: bool) -> int:
     procs = []
     for r in range(n):
         env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MCODEC_BENCH_CHILD="1")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MCODEC_BENCH_CHILD="1", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rcs = [None] * n
     failed_at = None
@@ -231,7 +231,24 @@ def scaling_fields(ranks: list, alg_bytes_per_rank: float, counted_bytes_per_ran
     }
 
 
-def dry_run(dist, rank: int, world: int, nchunks: int) -> None:
+def load_cpu(path: "str | None") -> "dict | None":
+    """The CPU baselines the launcher parent timed (MCODEC_BENCH_CPU_JSON)."""
+    if not path:
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def headline_cpu(cpu: "dict | None") -> "dict | None":
+    """The line's cpu_baseline: the C2 f32 restatement timed on this box."""
+    if not cpu or "C2_f32" not in cpu:
+        return None
+    c2 = dict(cpu["C2_f32"])
+    c2["sample"] = "Shuffle(4) enc+dec: " + c2["sample"]
+    return c2
+
+
+def dry_run(dist, rank: int, world: int, nchunks: int, cpu: "dict | None" = None) -> None:
     """CPU rehearsal of the sharded run (tests/test_distributed.py): every
     rank takes its contiguous C5 chunk range and encodes + verify-decodes a
     sample of its chunks with the oracle, timed between barriers like the GPU
@@ -259,7 +276,7 @@ def dry_run(dist, rank: int, world: int, nchunks: int) -> None:
     if rank == 0:
         covered = sorted(c for i in info for c in range(*i["range"]))
         line = {"dry_run": True, "max_over_ranks": t, "chunks": nchunks,
-                "covered_all": covered == list(range(nchunks))}
+                "covered_all": covered == list(range(nchunks)), "cpu_baseline": headline_cpu(cpu)}
         line.update(scaling_fields(info, 2 * 2 * 4096 * 3, 2 * 4096 * 3, t_max, on_gpu=False))
         print(json.dumps(line), flush=True)
 
@@ -277,11 +294,17 @@ CPU_CONFIGS = {  # config -> (single-core bytes, per-process bytes of the parall
 }
 
 
-def cpu_baselines(procs: int, seconds: float) -> dict:
+# the CPU legs an N > 1 run keeps (the headline's C2 f32 and the sharded C5)
+CPU_CONFIGS_MULTI = ("C2_f32", "C5")
+
+
+def cpu_baselines(procs: int, seconds: float, only=None) -> dict:
     from oracle import cpu_baseline as cb
 
     out = {}
     for cfg, (n1, npar) in CPU_CONFIGS.items():
+        if only is not None and cfg not in only:
+            continue
         one = cb.single_core(cfg, n1, seconds)
         if procs > 1:
             par = cb.parallel(cfg, procs, npar, seconds)
@@ -761,19 +784,42 @@ def main():
 
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, args.dry_run))
+        # the launcher parent never touches the GPU: it times the CPU legs
+        # (bounded: the headline's C2 f32 and C5) before it starts the ranks
+        # and hands them to rank 0 through a file
+        extra = {}
+        if not args.no_cpu:
+            import tempfile
+
+            cpu = cpu_baselines(args.cpu_procs, args.cpu_seconds, only=CPU_CONFIGS_MULTI)
+            fd, path = tempfile.mkstemp(prefix="mcodec_bench_cpu_", suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(cpu, f)
+            extra["MCODEC_BENCH_CPU_JSON"] = path
+        try:
+            rc = launch_ranks(args.gpus, args.dry_run, extra)
+        finally:
+            if extra:
+                os.unlink(extra["MCODEC_BENCH_CPU_JSON"])
+        sys.exit(rc)
     world_env = int(env_world or 1)
     if world_env != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world_env}")
 
-    # the CPU legs fork, so they run before anything touches the GPU
-    cpu = None
-    if world_env == 1 and not args.no_cpu and not args.dry_run:
-        cpu = cpu_baselines(args.cpu_procs, args.cpu_seconds)
+    # the CPU legs fork, so they run before anything touches the GPU: at N = 1
+    # all of them; at N > 1 the launcher parent's (self-launch) or, under
+    # torch.distributed.run, rank 0's own before it joins the process group
+    cpu = load_cpu(os.environ.get("MCODEC_BENCH_CPU_JSON"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    if cpu is None and rank_env == 0 and not args.no_cpu:
+        if world_env == 1 and not args.dry_run:
+            cpu = cpu_baselines(args.cpu_procs, args.cpu_seconds)
+        elif world_env > 1:
+            cpu = cpu_baselines(args.cpu_procs, args.cpu_seconds, only=CPU_CONFIGS_MULTI)
 
     dist, rank, world, local = dist_setup(args.dry_run)
     if args.dry_run:
-        dry_run(dist, rank, world, args.c5_chunks)
+        dry_run(dist, rank, world, args.c5_chunks, cpu)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -868,12 +914,19 @@ def main():
                 "ranks": c5_ranks,
             },
         }
-        if cpu is not None:
-            c2 = dict(cpu["C2_f32"])
-            c2["sample"] = "Shuffle(4) enc+dec: " + c2["sample"]
-            result["cpu_baseline"] = c2
-        else:
-            result["cpu_baseline"] = None
+        result["cpu_baseline"] = headline_cpu(cpu)
+        if world > 1:
+            # the N > 1 line keeps a bounded per-config block: the headline's
+            # C2 f32 (rank 0's launches) and the sharded C5, each beside its
+            # CPU baseline timed on this node before the ranks started
+            t_launch = launch_ms * 1e-3
+            result["cfg_C2_f32"] = _cfg(2 * CHUNK / GiB / (2 * t_launch), t_launch, t_launch, 4 * CHUNK,
+                                        "k_shuffle_enc<4> / k_shuffle4_dec_pair (rank 0, slowest launch)", cpu,
+                                        "C2_f32")
+            c5_call = c5_launch_ms * 1e-3
+            result["cfg_C5"] = _cfg(2 * c5_local * MiB / GiB / (2 * c5_call), c5_call, c5_call,
+                                    2 * c5_alg, "k_shuffle_f32_enc / k_f32_unshuffle (rank 0's chunk range)",
+                                    cpu, "C5", f"rank 0's {c5_local} of {args.c5_chunks} chunks per call")
         if world == 1 and not args.quick:
             result.update(config_workloads(dev, cpu))
             result["cfg_e2e"] = end_to_end(dev, cpu)

@@ -89,7 +89,15 @@ enum mc_dtype {
   MC_F2 = 9, /* '<f2' */
   MC_F4 = 10, /* '<f4' */
   MC_F8 = 11, /* '<f8' */
-  MC_NDTYPES = 12
+  MC_NDTYPES = 12,
+  /* extended dtypes (round 5): accepted by mc_cast / mc_cast_units,
+   * mc_delta_encode / mc_delta_decode (single chunk) and the FixedScaleOffset
+   * entry points; the batched and fused entry points refuse them (MC_EINVAL). */
+  MC_C8 = 12,  /* '<c8'  complex64: two f4 components (real, imag) */
+  MC_C16 = 13, /* '<c16' complex128: two f8 components */
+  MC_TD8 = 14, /* '<m8[unit]' timedelta64: int64 ticks, NaT = INT64_MIN */
+  MC_DT8 = 15, /* '<M8[unit]' datetime64: int64 ticks, NaT = INT64_MIN */
+  MC_NDTYPES_EXT = 16
 };
 
 int mc_abi_version(void);
@@ -137,7 +145,11 @@ int mc_bitround_shuffle(const void *src, void *dst, size_t n, int itemsize,
 
 /* ---- Delta ------------------------------------------------------------ */
 /* dst[0] = astype(src[0]); dst[i] = astype(src[i] - src[i-1]) computed in
- * dtype (bool: src[i] != src[i-1]).  n >= 1. */
+ * dtype (bool: src[i] != src[i-1]).  n >= 1.
+ * Extended dtypes: complex differences per component; timedelta / datetime
+ * differences are timedelta ticks with NaT propagation (NaT if either side
+ * is NaT, else the wrap-around difference), then cast to astype as
+ * mc_cast does (same unit). */
 int mc_delta_encode(const void *src, void *dst, size_t n, int dtype,
                     int astype, mc_stream_t stream);
 /* dst = cumsum(dtype(src)) accumulated in dtype (bool: logical or).  Integer
@@ -148,7 +160,16 @@ int mc_delta_encode(const void *src, void *dst, size_t n, int dtype,
  * the serial chain reruns from the first mismatch (bit-exact for any data;
  * smooth data verify entirely).  Otherwise (or with no workspace) float
  * decode is the serial chain.  The workspace's last 8 bytes hold the index
- * of the first mismatch (n if none) after the call. */
+ * of the first mismatch (n if none) after the call.
+ * Extended dtypes (the workspace is then required, MC_ENOSPC without it):
+ *  - dtype MC_TD8 from astype MC_TD8 / an integer / bool: numpy's timedelta
+ *    add loop -- the wrap-around prefix sum up to the first element that is
+ *    NaT or whose running sum is INT64_MIN, NaT from there on (an integer
+ *    scan plus a NaT pass); dtype MC_I8 from astype MC_TD8 likewise.
+ *  - complex dtype or astype: per component, the running sums of the real
+ *    and imaginary parts in the component type of promote(astype, dtype)
+ *    (each one mc_delta_decode of a real plane, so float speculation and
+ *    the serial chain apply per component), cast to dtype. */
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
 /* `ticket`: MC_ARRIVAL_WORDS device words (8-B aligned), zero before the
  * first call and left zero (one per stream): same-width integer decodes of
@@ -203,6 +224,38 @@ int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype,
  * float->int, correctly rounded float narrowing). */
 int mc_cast(const void *src, void *dst, size_t n, int from_dtype,
             int to_dtype, mc_stream_t stream);
+
+/* ---- extended dtypes: complex64/128, timedelta64, datetime64 ------------- */
+/* The codes carry no datetime unit: ticks are int64 in the caller's unit.
+ * numpy astype semantics (astype.py:46-58):
+ *  - complex -> complex: per-component float cast; complex -> bool: re != 0
+ *    or im != 0; complex -> other real: the real part cast (numpy's
+ *    ComplexWarning is the host's business); real -> complex: (x, +0).
+ *  - timedelta/datetime <-> int/float/bool/complex: the int64 ticks as an i8
+ *    (NaT is INT64_MIN like any other value; float -> ticks truncates with
+ *    x86-64 cvttsd2si, NaN/out of range -> INT64_MIN = NaT).
+ *  - time -> time: bits, or, with (num, den) != (1, 1) -- numpy's unit
+ *    conversion factor of a same-kind cast (m8 -> m8, M8 -> M8 between
+ *    linear units; the host computes it) -- NaT kept, else
+ *    v*num/den for v >= 0 and (v*num - (den - 1))/den for v < 0 (int64
+ *    wrap-around products, C division), as numpy's datetime cast loop does.
+ * mc_cast(...) == mc_cast_units(..., 1, 1). */
+int mc_cast_units(const void *src, void *dst, size_t n, int from_dtype,
+                  int to_dtype, int64_t num, int64_t den, mc_stream_t stream);
+/* FixedScaleOffset with complex compute dtypes (fixedscaleoffset.py:83-113):
+ * as mc_fso_encode / mc_fso_decode with complex scalars (re, im); integer
+ * compute dtypes take offset_i / scale_i.  Complex subtract/add are
+ * per component, multiply is (ar*br - ai*bi, ar*bi + ai*br) and divide is
+ * numpy's Smith-style loop (umath loops.c.src @TYPE@_divide), every scalar
+ * op rounded in the component type with x86-64 NaN propagation; rint per
+ * component.  The real entry points accept these codes too (imag parts 0). */
+int mc_fso_encode_x(const void *src, void *dst, size_t n, int dtype, int t1,
+                    int t2, int astype, double offset_re, double offset_im,
+                    int64_t offset_i, double scale_re, double scale_im,
+                    int64_t scale_i, mc_stream_t stream);
+int mc_fso_decode_x(const void *src, void *dst, size_t n, int astype, int t3,
+                    int t4, int dtype, double scale_re, double scale_im,
+                    double offset_re, double offset_im, mc_stream_t stream);
 
 /* ---- Fletcher32 ------------------------------------------------------- */
 size_t mc_fletcher32_workspace(size_t nbytes);

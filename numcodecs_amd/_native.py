@@ -50,6 +50,11 @@ DTYPE_CODES = {
 # bytes in registers (numpy normalises '>i1' / '>u1' / '>b1' to '|')
 MC_BIG_ENDIAN = 32
 DTYPE_CODES.update({">" + k[1:]: v | MC_BIG_ENDIAN for k, v in DTYPE_CODES.items() if k[0] == "<"})
+# extended dtypes (round 5): complex64/128, and timedelta64 / datetime64 of
+# any unit (the codes carry no unit: int64 ticks; unit casts take numpy's
+# conversion factor, see numcodecs_amd._ops.datetime_conversion_factor)
+MC_C8, MC_C16, MC_TD8, MC_DT8 = 12, 13, 14, 15
+EXT_CODES = {"c8": MC_C8, "c16": MC_C16, "m8": MC_TD8, "M8": MC_DT8}
 
 MC_OK = 0
 MC_EINVAL = -22
@@ -102,6 +107,14 @@ _SIGNATURES = {
     ],
     "mc_quantize": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_double, _c_vp],
     "mc_cast": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_vp],
+    "mc_cast_units": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_i64, _c_i64, _c_vp],
+    "mc_fso_encode_x": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int,
+        _c_double, _c_double, _c_i64, _c_double, _c_double, _c_i64, _c_vp,
+    ],
+    "mc_fso_decode_x": [
+        _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int, _c_double, _c_double, _c_double, _c_double, _c_vp,
+    ],
     "mc_fletcher32_workspace": [_c_size],
     "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],

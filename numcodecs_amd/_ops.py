@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import math
 import threading
 
 import numpy as np
@@ -22,16 +23,108 @@ __all__ = ["dtype_code", "stream", "workspace"]
 
 
 def dtype_code(dt) -> int:
-    """mc_dtype code of numpy dtype `dt`: bool/int/uint/float of either byte
-    order (a big-endian dtype carries MC_BIG_ENDIAN)."""
+    """mc_dtype code of numpy dtype `dt`: bool/int/uint/float/complex and
+    timedelta64/datetime64 (any unit) of either byte order (a big-endian
+    dtype carries MC_BIG_ENDIAN)."""
     dt = np.dtype(dt)
-    try:
-        return DTYPE_CODES[dt.str]
-    except KeyError:
+    code = DTYPE_CODES.get(dt.str)
+    if code is not None:
+        return code
+    key = "m8" if dt.kind == "m" else "M8" if dt.kind == "M" else dt.str[1:]
+    code = _native.EXT_CODES.get(key) if dt.kind in "cmM" else None
+    if code is None:
         raise NotImplementedError(
             f"dtype {dt.str!r} is not supported by the numcodecs_amd device kernels "
-            "(bool/int/uint/float only)"
-        ) from None
+            "(bool/int/uint/float/complex/timedelta64/datetime64 only)"
+        )
+    return code | (_native.MC_BIG_ENDIAN if dt.byteorder == ">" else 0)
+
+
+def is_ext_dtype(dt) -> bool:
+    """complex, timedelta64 or datetime64: the dtypes computed by mc_ext.hip."""
+    return np.dtype(dt).kind in "cmM"
+
+
+# numpy's datetime unit table (datetime.c: NPY_DATETIMEUNIT order and
+# _datetime_factors), restated for get_datetime_conversion_factor
+_DT_UNITS = ["Y", "M", "W", "D", "h", "m", "s", "ms", "us", "ns", "ps", "fs", "as"]
+_DT_FACTORS = [1, 1, 7, 24, 60, 60, 1000, 1000, 1000, 1000, 1000, 1000, 1]
+_U64 = (1 << 64) - 1
+
+
+def _units_factor(big: int, little: int) -> int:
+    """get_datetime_units_factor: ticks of unit `little` per unit `big`
+    (0 on overflow, as numpy)."""
+    f = 1
+    for u in range(big, little):
+        f = (f * _DT_FACTORS[u]) & _U64
+        if f & 0xFF00000000000000:
+            return 0
+    return f
+
+
+def datetime_conversion_factor(src, dst) -> "tuple[int, int]":
+    """(num, den) of numpy's get_datetime_conversion_factor between the units
+    of two timedelta64/datetime64 dtypes (reduced), so that a same-kind cast
+    is v*num/den with numpy's floor rounding of negatives (mc_cast_units).
+    Generic source units convert with (1, 1); specific -> generic raises
+    like numpy."""
+    su, sn = np.datetime_data(np.dtype(src))
+    du, dn = np.datetime_data(np.dtype(dst))
+    if su == "generic":
+        return 1, 1
+    if du == "generic":
+        raise ValueError("Cannot convert from specific units to generic units in NumPy datetimes or timedeltas")
+    sb, db = _DT_UNITS.index(su), _DT_UNITS.index(du)
+    swapped = sb > db
+    lo, hi = (db, sb) if swapped else (sb, db)
+    num = den = 1
+    if lo != hi:
+        ylen = 97 + 400 * 365
+        if lo == 0:  # years
+            if hi == 1:
+                num *= 12
+            elif hi == 2:
+                num, den = num * ylen, den * 400 * 7
+            else:
+                num, den = num * ylen * _units_factor(3, hi), den * 400
+        elif lo == 1:  # months
+            if hi == 2:
+                num, den = num * ylen, den * 400 * 12 * 7
+            else:
+                num, den = num * ylen * _units_factor(3, hi), den * 400 * 12
+        else:
+            num *= _units_factor(lo, hi)
+    num &= _U64
+    if num == 0:
+        raise OverflowError(
+            "Integer overflow while computing the conversion factor between NumPy datetime units "
+            f"{_DT_UNITS[lo]} and {_DT_UNITS[hi]}")
+    if swapped:
+        num, den = den, num
+    num, den = (num * sn) & _U64, (den * dn) & _U64
+    g = math.gcd(num, den)
+    return num // g, den // g
+
+
+def time_cast_factor(from_dt, to_dt) -> "tuple[int, int]":
+    """The (num, den) mc_cast_units applies for numpy's astype(from -> to):
+    a unit conversion between two timedelta64 or two datetime64 dtypes
+    (linear units), (1, 1) otherwise (a timedelta <-> datetime cast keeps the
+    ticks, as numpy's does).  Calendar conversions of datetime64 between
+    years/months and the other units are not implemented."""
+    f, t = np.dtype(from_dt), np.dtype(to_dt)
+    if f.kind not in "mM" or t.kind != f.kind:
+        return 1, 1
+    if np.datetime_data(f) == np.datetime_data(t):
+        return 1, 1
+    if f.kind == "M":
+        fu, tu = np.datetime_data(f)[0], np.datetime_data(t)[0]
+        if (fu in ("Y", "M")) != (tu in ("Y", "M")) and "generic" not in (fu, tu):
+            raise NotImplementedError(
+                f"calendar datetime64 conversion {f.str!r} -> {t.str!r} is not supported by the numcodecs_amd "
+                "device kernels")
+    return datetime_conversion_factor(f, t)
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
@@ -273,13 +366,29 @@ def _scalar_args(value, dt):
     return 0.0, int(arr)
 
 
+def _complex_args(value, dt):
+    """(re, im, int64) triple carrying `value` in compute dtype `dt`."""
+    if np.dtype(dt).kind == "c":
+        v = complex(np.asarray(value).astype(dt))
+        return v.real, v.imag, 0
+    f, i = _scalar_args(value, dt)
+    return f, 0.0, i
+
+
 def fso_encode(src, dst, n, dtype, t1, t2, astype, offset_t1, scale_t2) -> None:
     _native.require_device()
     if n == 0:
         return
-    of, oi = _scalar_args(offset_t1, t1)
-    sf, si = _scalar_args(scale_t2, t2)
     with _guard(src):
+        if any(is_ext_dtype(t) for t in (dtype, t1, t2, astype)):
+            ore, oim, oi = _complex_args(offset_t1, t1)
+            sre, sim, si = _complex_args(scale_t2, t2)
+            check(lib.mc_fso_encode_x(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype), dtype_code(t1),
+                                      dtype_code(t2), dtype_code(astype), ore, oim, oi, sre, sim, si,
+                                      stream(src)), "mc_fso_encode_x")
+            return
+        of, oi = _scalar_args(offset_t1, t1)
+        sf, si = _scalar_args(scale_t2, t2)
         check(lib.mc_fso_encode(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype), dtype_code(t1),
                                 dtype_code(t2), dtype_code(astype), of, oi, sf, si, stream(src)),
               "mc_fso_encode")
@@ -290,6 +399,13 @@ def fso_decode(src, dst, n, astype, t3, t4, dtype, scale_t3, offset_t4) -> None:
     if n == 0:
         return
     with _guard(src):
+        if any(is_ext_dtype(t) for t in (astype, t3, t4, dtype)):
+            sre, sim, _ = _complex_args(scale_t3, t3)
+            ore, oim, _ = _complex_args(offset_t4, t4)
+            check(lib.mc_fso_decode_x(src.data_ptr(), dst.data_ptr(), n, dtype_code(astype), dtype_code(t3),
+                                      dtype_code(t4), dtype_code(dtype), sre, sim, ore, oim, stream(src)),
+                  "mc_fso_decode_x")
+            return
         check(lib.mc_fso_decode(src.data_ptr(), dst.data_ptr(), n, dtype_code(astype), dtype_code(t3),
                                 dtype_code(t4), dtype_code(dtype), float(scale_t3), float(offset_t4),
                                 stream(src)), "mc_fso_decode")
@@ -305,10 +421,17 @@ def quantize(src, dst, n, dtype, astype, scale) -> None:
 
 
 def cast(src, dst, n, from_dt, to_dt) -> None:
+    """numpy astype(from_dt -> to_dt) of n elements; timedelta64/datetime64
+    unit conversions take numpy's conversion factor (mc_cast_units)."""
     _native.require_device()
     if n == 0:
         return
     with _guard(src):
+        if is_ext_dtype(from_dt) or is_ext_dtype(to_dt):
+            num, den = time_cast_factor(from_dt, to_dt)
+            check(lib.mc_cast_units(src.data_ptr(), dst.data_ptr(), n, dtype_code(from_dt), dtype_code(to_dt),
+                                    num, den, stream(src)), "mc_cast_units")
+            return
         check(lib.mc_cast(src.data_ptr(), dst.data_ptr(), n, dtype_code(from_dt), dtype_code(to_dt),
                           stream(src)), "mc_cast")
 

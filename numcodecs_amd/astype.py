@@ -22,6 +22,11 @@ def _cast(buf, from_dt, to_dt, out=None):
     """The cast, written straight into a device `out` when it can take it
     (then `out` is returned, else the new array)."""
     src = to_dbuf(buf, flatten=False, contiguous=False)
+    if from_dt != to_dt and (_ops.is_ext_dtype(from_dt) or _ops.is_ext_dtype(to_dt)):
+        # numpy's own errors / ComplexWarning, as astype.py:53,58 raise them,
+        # and its result dtype (a cast to generic timedelta64 / datetime64
+        # keeps the source unit)
+        to_dt = np.zeros(1, dtype=from_dt).astype(to_dt).dtype
     if src.nbytes % from_dt.itemsize:
         raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
     n = src.nbytes // from_dt.itemsize
@@ -30,6 +35,8 @@ def _cast(buf, from_dt, to_dt, out=None):
     dst = empty_like_bytes(n * to_dt.itemsize, src) if direct is None else direct
     if from_dt == to_dt:
         _ops.copy(src.data, dst, src.nbytes)
+    elif _ops.is_ext_dtype(from_dt) or _ops.is_ext_dtype(to_dt):
+        _ops.cast(src.data, dst, n, from_dt, to_dt)
     else:
         _ops.cast(src.data, dst, n, from_dt, to_dt)
     if direct is not None:

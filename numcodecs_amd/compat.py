@@ -55,6 +55,8 @@ _NP_TO_TORCH = {
     "<f2": torch.float16,
     "<f4": torch.float32,
     "<f8": torch.float64,
+    "<c8": torch.complex64,
+    "<c16": torch.complex128,
 }
 _TORCH_TO_NP = {v: np.dtype(k) for k, v in _NP_TO_TORCH.items()}
 

@@ -449,3 +449,13 @@ MC_HD uint64_t mc_cvtt_u64(double x) {  // gcc's unsigned sequence (no AVX-512)
   if (!(x >= 9223372036854775808.0)) return (uint64_t)mc_cvtt_i64(x);
   return (uint64_t)mc_cvtt_i64(x - 9223372036854775808.0) ^ 0x8000000000000000ull;
 }
+
+// ---------------------------------------------------------------------------
+// extended dtypes (mc_ext.hip): complex64/128, timedelta64, datetime64.  The
+// real entry points route these codes here (C++ linkage).
+// ---------------------------------------------------------------------------
+bool mc_ext_code(int dt);  // a valid MC_C8 / MC_C16 / MC_TD8 / MC_DT8 code (either byte order)
+int mc_ext_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype, hipStream_t st);
+size_t mc_ext_delta_decode_workspace(size_t n, int astype, int dtype);
+int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
+                        size_t workspace_bytes, uint32_t *ticket, hipStream_t st);

@@ -503,6 +503,12 @@ int mc_bitround(const void *src, void *dst, size_t n, int itemsize, int keepbits
 
 int mc_cast(const void *src, void *dst, size_t n, int from_dtype, int to_dtype,
             mc_stream_t stream) {
+  // extended dtypes, and casts that only change byte order (a pure byte
+  // reversal: the value kernel's float -> double -> float round trip would
+  // quiet signalling NaNs, which numpy's byte-swapping cast keeps)
+  if (mc_ext_code(from_dtype) || mc_ext_code(to_dtype) ||
+      (mc_valid_dtype(from_dtype) && mc_valid_dtype(to_dtype) && mc_dt_base(from_dtype) == mc_dt_base(to_dtype)))
+    return mc_cast_units(src, dst, n, from_dtype, to_dtype, 1, 1, stream);
   // compute dtypes are native: the byte order lives in the input/output codes
   const int fb = mc_dt_base(from_dtype);
   MapParams p{from_dtype, fb, fb, to_dtype, McNum{0, 0}, McNum{0, 0}};
@@ -512,6 +518,9 @@ int mc_cast(const void *src, void *dst, size_t n, int from_dtype, int to_dtype,
 int mc_fso_encode(const void *src, void *dst, size_t n, int dtype, int t1, int t2, int astype,
                   double offset_f, int64_t offset_i, double scale_f, int64_t scale_i,
                   mc_stream_t stream) {
+  if (mc_ext_code(dtype) || mc_ext_code(t1) || mc_ext_code(t2) || mc_ext_code(astype))
+    return mc_fso_encode_x(src, dst, n, dtype, t1, t2, astype, offset_f, 0.0, offset_i, scale_f, 0.0, scale_i,
+                           stream);
   MapParams p{dtype, t1, t2, astype, num_scalar(t1, offset_f, offset_i),
               num_scalar(t2, scale_f, scale_i)};
   return launch_map<K_FSO_ENC>(src, dst, n, p, (hipStream_t)stream);
@@ -519,6 +528,8 @@ int mc_fso_encode(const void *src, void *dst, size_t n, int dtype, int t1, int t
 
 int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3, int t4, int dtype,
                   double scale, double offset, mc_stream_t stream) {
+  if (mc_ext_code(dtype) || mc_ext_code(t3) || mc_ext_code(t4) || mc_ext_code(astype))
+    return mc_fso_decode_x(src, dst, n, astype, t3, t4, dtype, scale, 0.0, offset, 0.0, stream);
   if (!mc_is_float(t3) || !mc_is_float(t4)) return MC_EINVAL;
   MapParams p{astype, t3, t4, dtype, num_scalar(t3, scale, 0), num_scalar(t4, offset, 0)};
   // integer inputs (exact in f64) divided in f64 by the constant scale
@@ -548,6 +559,9 @@ int mc_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype,
 
 int mc_delta_encode_batch(const void *src, size_t src_stride, void *dst, size_t dst_stride,
                           size_t nchunks, size_t n, int dtype, int astype, mc_stream_t stream) {
+  if (mc_ext_code(dtype) || mc_ext_code(astype))  // extended dtypes: single chunks only
+    return nchunks == 1 ? mc_ext_delta_encode(src, dst, n, dtype, astype, (hipStream_t)stream)
+                        : (nchunks == 0 ? MC_OK : MC_EINVAL);
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
   if (n == 0 || nchunks == 0) return MC_OK;
   if (!src || !dst) return MC_EINVAL;

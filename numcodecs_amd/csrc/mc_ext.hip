@@ -1,0 +1,733 @@
+// mc_ext.hip -- the extended dtypes of the elementwise codecs on gfx950:
+// complex64 / complex128, timedelta64 and datetime64 (round 5).
+//
+//   mc_cast_units   ndarray.astype (astype.py:46-58) incl. datetime unit casts
+//   mc_fso_*_x      fixedscaleoffset.py:83-113 with complex compute dtypes
+//   Delta encode    delta.py:52-67 (np.diff): complex per component, timedelta
+//                   with NaT propagation, datetime - datetime -> timedelta
+//   Delta decode    delta.py:69-83 (np.cumsum): timedelta = integer scan + NaT
+//                   pass; complex = one real decode per component plane
+//
+// numpy computes these dtypes with the same scalar C loops as the real ones
+// (umath loops.c.src: complex add/subtract per component, multiply
+// (ar*br - ai*bi, ar*bi + ai*br), divide by Smith's method; TIMEDELTA_mm_m_add
+// / _subtract and DATETIME_MM_m_subtract return NaT when an operand is NaT,
+// else the int64 result), so every scalar op below is one IEEE op in the
+// component type with numpy's x86-64 NaN choice (mc_x86_nan via
+// mc_num_binop) or one wrap-around int64 op.  These dtypes are off the
+// BASELINE path: the kernels move one element per lane per step
+// (lane-contiguous 8- / 16-B accesses), correctness first.
+#include "mc_num.h"
+
+namespace {
+
+MC_HD bool x_is_complex(int dt) {
+  const int b = mc_dt_base(dt);
+  return b == MC_C8 || b == MC_C16;
+}
+MC_HD bool x_is_time(int dt) {
+  const int b = mc_dt_base(dt);
+  return b == MC_TD8 || b == MC_DT8;
+}
+MC_HD bool x_is_ext(int dt) { return mc_dt_base(dt) >= MC_NDTYPES; }
+// component dtype of a complex code (byte order kept: each component of a
+// '>c8' is a big-endian f4)
+MC_HD int x_comp(int dt) {
+  return (mc_dt_base(dt) == MC_C8 ? MC_F4 : MC_F8) | (dt & MC_BIG_ENDIAN);
+}
+// the real dtype a non-complex code computes as: time ticks are int64
+MC_HD int x_real(int dt) { return x_is_time(dt) ? (MC_I8 | (dt & MC_BIG_ENDIAN)) : dt; }
+MC_HD int x_itemsize(int dt) {
+  switch (mc_dt_base(dt)) {
+    case MC_C8: case MC_TD8: case MC_DT8: return 8;
+    case MC_C16: return 16;
+    default: return mc_itemsize(dt);
+  }
+}
+static inline bool x_valid(int dt) {
+  const int b = mc_dt_base(dt);
+  return b >= 0 && b < MC_NDTYPES_EXT && (dt & ~(MC_BIG_ENDIAN | 31)) == 0 &&
+         (!mc_dt_swapped(dt) || x_itemsize(b) > 1);
+}
+
+constexpr int64_t NAT = INT64_MIN;
+
+// a value of any dtype: real part / integer / ticks in `re` (McNum), the
+// imaginary part of a complex in `im`
+struct McX {
+  McNum re;
+  double im;
+};
+
+MC_HD McX x_make(McNum re, double im = 0.0) {
+  McX r;
+  r.re = re;
+  r.im = im;
+  return r;
+}
+
+// element idx of dtype dt at p: `al` = p is aligned to the element's
+// component size (else byte loads)
+MC_DEV uint64_t x_ld(const uint8_t *p, size_t byte_off, int size, bool al) {
+  return al ? mc_load_elem(p + byte_off, 0, size) : mc_load_elem_u(p + byte_off, 0, size);
+}
+MC_DEV void x_st(uint8_t *p, size_t byte_off, int size, uint64_t v, bool al) {
+  if (al) mc_store_elem(p + byte_off, 0, size, v);
+  else mc_store_elem_u(p + byte_off, 0, size, v);
+}
+
+MC_DEV McX x_load(const uint8_t *p, size_t idx, int dt, bool al) {
+  if (x_is_complex(dt)) {
+    const int c = x_comp(dt), cs = mc_itemsize(c);
+    const size_t o = idx * 2 * (size_t)cs;
+    return x_make(mc_num_from_bits(x_ld(p, o, cs, al), c), mc_num_from_bits(x_ld(p, o + cs, cs, al), c).f);
+  }
+  const int r = x_real(dt), s = mc_itemsize(r);
+  return x_make(mc_num_from_bits(x_ld(p, idx * (size_t)s, s, al), r));
+}
+
+MC_DEV void x_store(uint8_t *p, size_t idx, int dt, const McX &v, bool al) {
+  if (x_is_complex(dt)) {
+    const int c = x_comp(dt), cs = mc_itemsize(c);
+    const size_t o = idx * 2 * (size_t)cs;
+    x_st(p, o, cs, mc_num_to_bits(v.re, c), al);
+    x_st(p, o + cs, cs, mc_num_to_bits(mc_num_f(v.im), c), al);
+    return;
+  }
+  const int r = x_real(dt), s = mc_itemsize(r);
+  x_st(p, idx * (size_t)s, s, mc_num_to_bits(v.re, r), al);
+}
+
+// numpy's datetime unit cast (datetime.c, _strided_to_strided_datetime_cast)
+MC_DEV int64_t x_scale_ticks(int64_t v, int64_t num, int64_t den) {
+  if (v == NAT || (num == 1 && den == 1)) return v;
+  const int64_t m = (int64_t)((uint64_t)v * (uint64_t)num);  // wraps as numpy's does
+  return v < 0 ? (int64_t)((uint64_t)m - (uint64_t)(den - 1)) / den : m / den;
+}
+
+// numpy astype(from -> to), unsafe casting
+MC_DEV McX x_cast(const McX &v, int from, int to, int64_t num, int64_t den) {
+  if (x_is_complex(from)) {
+    const int fc = mc_dt_base(x_comp(from));
+    if (x_is_complex(to)) {
+      const int tc = mc_dt_base(x_comp(to));
+      return x_make(mc_num_cast(v.re, fc, tc), mc_num_cast(mc_num_f(v.im), fc, tc).f);
+    }
+    if (mc_dt_base(to) == MC_B1) return x_make(mc_num_i(v.re.f != 0.0 || v.im != 0.0));
+    return x_make(mc_num_cast(v.re, fc, mc_dt_base(x_real(to))));  // the real part
+  }
+  if (x_is_complex(to)) return x_make(mc_num_cast(v.re, mc_dt_base(x_real(from)), mc_dt_base(x_comp(to))), 0.0);
+  if (x_is_time(from) && x_is_time(to)) return x_make(mc_num_i(x_scale_ticks(v.re.i, num, den)));
+  return x_make(mc_num_cast(v.re, mc_dt_base(x_real(from)), mc_dt_base(x_real(to))));
+}
+
+// component-wise op of a complex dtype / NaT-aware op of a time dtype / the
+// real op
+MC_DEV McX x_addsub(const McX &a, const McX &b, int op, int dt) {
+  if (x_is_complex(dt)) {
+    const int c = mc_dt_base(x_comp(dt));
+    return x_make(mc_num_binop(a.re, b.re, op, c), mc_num_binop(mc_num_f(a.im), mc_num_f(b.im), op, c).f);
+  }
+  if (x_is_time(dt)) {
+    if (a.re.i == NAT || b.re.i == NAT) return x_make(mc_num_i(NAT));
+    const uint64_t x = (uint64_t)a.re.i, y = (uint64_t)b.re.i;
+    return x_make(mc_num_i((int64_t)(op == MC_OP_ADD ? x + y : x - y)));
+  }
+  return x_make(mc_num_binop(a.re, b.re, op, dt));
+}
+
+MC_DEV double x_op(double a, double b, int op, int c) { return mc_num_binop(mc_num_f(a), mc_num_f(b), op, c).f; }
+
+MC_DEV double x_fabs(double a) { return __builtin_fabs(a); }
+
+MC_DEV McX x_mul(const McX &a, const McX &b, int dt) {
+  if (!x_is_complex(dt)) return x_make(mc_num_binop(a.re, b.re, MC_OP_MUL, dt));
+  const int c = mc_dt_base(x_comp(dt));
+  const double ar = a.re.f, ai = a.im, br = b.re.f, bi = b.im;
+  const double re = x_op(x_op(ar, br, MC_OP_MUL, c), x_op(ai, bi, MC_OP_MUL, c), MC_OP_SUB, c);
+  const double im = x_op(x_op(ar, bi, MC_OP_MUL, c), x_op(ai, br, MC_OP_MUL, c), MC_OP_ADD, c);
+  return x_make(mc_num_f(re), im);
+}
+
+// numpy's complex divide (umath loops.c.src @TYPE@_divide)
+MC_DEV McX x_div(const McX &a, const McX &b, int dt) {
+  if (!x_is_complex(dt)) return x_make(mc_num_binop(a.re, b.re, MC_OP_DIV, dt));
+  const int c = mc_dt_base(x_comp(dt));
+  const double ar = a.re.f, ai = a.im, br = b.re.f, bi = b.im;
+  const double abr = x_fabs(br), abi = x_fabs(bi);
+  double re, im;
+  if (abr >= abi) {
+    if (abr == 0.0 && abi == 0.0) {
+      re = x_op(ar, abr, MC_OP_DIV, c);
+      im = x_op(ai, abr, MC_OP_DIV, c);
+    } else {
+      const double rat = x_op(bi, br, MC_OP_DIV, c);
+      const double scl = x_op(1.0, x_op(br, x_op(bi, rat, MC_OP_MUL, c), MC_OP_ADD, c), MC_OP_DIV, c);
+      re = x_op(x_op(ar, x_op(ai, rat, MC_OP_MUL, c), MC_OP_ADD, c), scl, MC_OP_MUL, c);
+      im = x_op(x_op(ai, x_op(ar, rat, MC_OP_MUL, c), MC_OP_SUB, c), scl, MC_OP_MUL, c);
+    }
+  } else {
+    const double rat = x_op(br, bi, MC_OP_DIV, c);
+    const double scl = x_op(1.0, x_op(bi, x_op(br, rat, MC_OP_MUL, c), MC_OP_ADD, c), MC_OP_DIV, c);
+    re = x_op(x_op(x_op(ar, rat, MC_OP_MUL, c), ai, MC_OP_ADD, c), scl, MC_OP_MUL, c);
+    im = x_op(x_op(x_op(ai, rat, MC_OP_MUL, c), ar, MC_OP_SUB, c), scl, MC_OP_MUL, c);
+  }
+  return x_make(mc_num_f(re), im);
+}
+
+MC_DEV McX x_rint(const McX &v, int dt) {
+  if (!x_is_complex(dt)) return x_make(mc_num_rint(v.re, dt));
+  const int c = mc_dt_base(x_comp(dt));
+  return x_make(mc_num_rint(v.re, c), mc_num_rint(mc_num_f(v.im), c).f);
+}
+
+enum XKind { X_CAST = 0, X_FSO_ENC = 1, X_FSO_DEC = 2 };
+
+struct XParams {
+  int d, t1, t2, a;  // input dtype, compute dtypes, output dtype
+  McX s0, s1;        // scalars in their compute dtypes
+  int64_t num, den;  // unit conversion (X_CAST between time dtypes)
+  bool al;           // both buffers aligned to their component sizes
+};
+
+constexpr int X_STEPS = 4;  // elements per thread
+
+template <int KIND>
+__global__ __launch_bounds__(MC_BLOCK) void k_xmap(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                  size_t n, XParams p) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i >= n) return;
+    McX v = x_load(src, i, p.d, p.al);
+    if constexpr (KIND == X_CAST) {
+      v = x_cast(v, p.d, p.a, p.num, p.den);
+    } else if constexpr (KIND == X_FSO_ENC) {  // astype(rint((x - offset) * scale))
+      v = x_cast(v, p.d, p.t1, 1, 1);
+      v = x_addsub(v, p.s0, MC_OP_SUB, p.t1);
+      v = x_cast(v, p.t1, p.t2, 1, 1);
+      v = x_mul(v, p.s1, p.t2);
+      v = x_rint(v, p.t2);
+      v = x_cast(v, p.t2, p.a, 1, 1);
+    } else {  // X_FSO_DEC: dtype((x / scale) + offset)
+      v = x_cast(v, p.d, p.t1, 1, 1);
+      v = x_div(v, p.s0, p.t1);
+      v = x_cast(v, p.t1, p.t2, 1, 1);
+      v = x_addsub(v, p.s1, MC_OP_ADD, p.t2);
+      v = x_cast(v, p.t2, p.a, 1, 1);
+    }
+    x_store(dst, i, p.a, v, p.al);
+  }
+}
+
+// Delta encode: y[0] = astype(x[0]); y[i] = astype(x[i] - x[i-1]), the
+// difference in dtype (datetime - datetime = timedelta ticks)
+__global__ __launch_bounds__(MC_BLOCK) void k_xdelta_enc(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                        size_t n, int d, int a, bool al) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  const int diff_dt = mc_dt_base(d) == MC_DT8 ? MC_TD8 : mc_dt_base(d);
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i >= n) return;
+    const McX x = x_load(src, i, d, al);
+    McX y;
+    if (i == 0) y = x_cast(x, d, a, 1, 1);
+    else y = x_cast(x_addsub(x, x_load(src, i - 1, d, al), MC_OP_SUB, diff_dt), diff_dt, a, 1, 1);
+    x_store(dst, i, a, y, al);
+  }
+}
+
+// complex -> two native component planes
+__global__ __launch_bounds__(MC_BLOCK) void k_xsplit(const uint8_t *__restrict__ src, uint8_t *__restrict__ re,
+                                                    uint8_t *__restrict__ im, size_t n, int dt, bool al) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  const int c = x_comp(dt), cs = mc_itemsize(c);
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i >= n) return;
+    const size_t o = i * 2 * (size_t)cs;
+    // raw component bits, byte order normalised: no value conversion
+    mc_store_elem(re, i, cs, mc_to_storage(x_ld(src, o, cs, al), c));
+    mc_store_elem(im, i, cs, mc_to_storage(x_ld(src, o + cs, cs, al), c));
+  }
+}
+
+// two native planes of component dtype lc (im may be NULL: +0) as the
+// complex of that component type, cast to dtype
+__global__ __launch_bounds__(MC_BLOCK) void k_xmerge(const uint8_t *__restrict__ re, const uint8_t *__restrict__ im,
+                                                    uint8_t *__restrict__ dst, size_t n, int lc, int dt,
+                                                    bool al) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  const int loop = lc == MC_F4 ? MC_C8 : MC_C16;
+  const int cs = mc_itemsize(lc);
+  // the same component type: the sums' bits moved as they are (a signalling
+  // NaN kept, as numpy's cast of the running sums keeps it)
+  const bool bits = x_is_complex(dt) && mc_dt_base(x_comp(dt)) == lc;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i >= n) return;
+    if (bits) {
+      const int c = x_comp(dt);
+      x_st(dst, i * 2 * (size_t)cs, cs, mc_to_storage(mc_load_elem(re, i, cs), c), al);
+      x_st(dst, i * 2 * (size_t)cs + cs, cs, im ? mc_to_storage(mc_load_elem(im, i, cs), c) : 0, al);
+      continue;
+    }
+    const McX v = x_make(mc_num_from_bits(mc_load_elem(re, i, cs), lc),
+                         im ? mc_num_from_bits(mc_load_elem(im, i, cs), lc).f : 0.0);
+    x_store(dst, i, dt, x_cast(v, loop, dt, 1, 1), al);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// numpy's complex add loops pick the SECOND operand's NaN when both are NaN
+// for complex64 (and for complex128 when the accumulate has 2 elements),
+// the first one for complex128 (complex64 at 2 elements) -- measured on the
+// reference's numpy (tests/golden/make_golden_ext.py, NaN + NaN cumsums);
+// the real chains (mc_scan.h ser_add) use the first.  Once a running sum is
+// NaN it stays NaN, so the second-operand rule only changes the NaN tail:
+// every sum from the first NaN input at or after the tail's start on is that
+// input's NaN quieted (in the loop type), up to the next NaN input.  Three
+// passes over one component plane: per-block last NaN input, an exclusive
+// max-scan over blocks, and the rewrite of NaN sums (blocks with no NaN
+// input at or before them exit before reading anything).
+// ---------------------------------------------------------------------------
+constexpr int NF_BLOCK = 4096;  // elements per block (16 per thread)
+
+MC_DEV bool x_is_nan_bits(uint64_t b, int c) {
+  switch (mc_dt_base(c)) {
+    case MC_F2: return (b & 0x7fffu) > 0x7c00u;
+    case MC_F4: return (b & 0x7fffffffu) > 0x7f800000u;
+    case MC_F8: return (b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+    default: return false;  // integers / bool never are
+  }
+}
+
+__global__ __launch_bounds__(MC_BLOCK) void k_nanfix_last(const uint8_t *__restrict__ in, int ac, size_t n,
+                                                         long long *__restrict__ last) {
+  __shared__ long long red[MC_BLOCK / 64];
+  const size_t b0 = (size_t)blockIdx.x * NF_BLOCK;
+  const int es = mc_itemsize(ac);
+  long long m = -1;
+  for (size_t i = b0 + threadIdx.x; i < n && i < b0 + NF_BLOCK; i += MC_BLOCK)
+    if (x_is_nan_bits(mc_load_elem(in, i, es), ac)) m = (long long)i;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const long long o = __shfl_xor(m, off);
+    m = o > m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long r = red[0];
+    for (int w = 1; w < MC_BLOCK / 64; ++w) r = red[w] > r ? red[w] : r;
+    last[blockIdx.x] = r;
+  }
+}
+
+// carry[b] = max(last[0..b)) (exclusive), one workgroup, nb values
+__global__ __launch_bounds__(MC_BLOCK) void k_nanfix_scan(const long long *__restrict__ last,
+                                                         long long *__restrict__ carry, size_t nb) {
+  __shared__ long long tot[MC_BLOCK];
+  // thread t owns the contiguous range [t*per, (t+1)*per)
+  const size_t per = (nb + MC_BLOCK - 1) / MC_BLOCK;
+  const size_t t0 = threadIdx.x * per;
+  long long m = -1;
+  for (size_t b = t0; b < nb && b < t0 + per; ++b) m = last[b] > m ? last[b] : m;
+  tot[threadIdx.x] = m;
+  __syncthreads();
+  long long c = -1;
+  for (unsigned t = 0; t < threadIdx.x; ++t) c = tot[t] > c ? tot[t] : c;
+  for (size_t b = t0; b < nb && b < t0 + per; ++b) {
+    carry[b] = c;
+    c = last[b] > c ? last[b] : c;
+  }
+}
+
+__global__ __launch_bounds__(MC_BLOCK) void k_nanfix_apply(const uint8_t *__restrict__ in, int ac,
+                                                          uint8_t *__restrict__ out, int lc, size_t n,
+                                                          const long long *__restrict__ last,
+                                                          const long long *__restrict__ carry) {
+  const size_t b0 = (size_t)blockIdx.x * NF_BLOCK;
+  const long long cin = carry[blockIdx.x];
+  if (cin < 0 && last[blockIdx.x] < 0) return;  // no NaN input up to this block's end
+  __shared__ long long wmax[MC_BLOCK / 64];
+  const int es = mc_itemsize(ac), os = mc_itemsize(lc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // thread t owns the 16 consecutive elements [b0 + 16t, b0 + 16t + 16)
+  constexpr int PER = NF_BLOCK / MC_BLOCK;
+  const size_t e0 = b0 + (size_t)threadIdx.x * PER;
+  long long mine = -1;
+  for (int k = 0; k < PER; ++k)
+    if (e0 + k < n && x_is_nan_bits(mc_load_elem(in, e0 + k, es), ac)) mine = (long long)(e0 + k);
+  // exclusive prefix max over the block's threads: wave scan + wave totals
+  long long incl = mine;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const long long o = __shfl_up(incl, off);
+    if (lane >= off) incl = o > incl ? o : incl;
+  }
+  if (lane == 63) wmax[wave] = incl;
+  __syncthreads();
+  long long j = __shfl_up(incl, 1);
+  if (lane == 0) j = -1;
+  for (int w = 0; w < wave; ++w) j = wmax[w] > j ? wmax[w] : j;
+  j = cin > j ? cin : j;
+  for (int k = 0; k < PER; ++k) {
+    const size_t i = e0 + k;
+    if (i >= n) break;
+    const uint64_t e = mc_load_elem(in, i, es);
+    if (x_is_nan_bits(e, ac)) j = (long long)i;
+    if (j < 0) continue;
+    const uint64_t sb = mc_load_elem(out, i, os);
+    if (!x_is_nan_bits(sb, lc)) continue;
+    // the NaN input at j in the loop type, quieted (numpy's cast then add)
+    const uint64_t eb = mc_load_elem(in, (size_t)j, es);
+    uint64_t v;
+    if (mc_dt_base(lc) == MC_F4) {
+      const uint32_t f = mc_dt_base(ac) == MC_F2 ? mc_half_to_float_bits((uint16_t)eb) : (uint32_t)eb;
+      v = f | 0x00400000u;
+    } else {  // f8 sums: from f2 / f4 / f8 inputs (IEEE widening keeps the payload's top bits)
+      const uint64_t w = mc_dt_base(ac) == MC_F8 ? eb
+                         : mc_dt_base(ac) == MC_F4 ? mc_f64_bits((double)mc_bits_f32((uint32_t)eb | 0x00400000u))
+                                                   : mc_f64_bits((double)mc_half_to_float(((uint16_t)eb) | 0x0200u));
+      v = w | 0x0008000000000000ull;
+    }
+    mc_store_elem(out, i, os, v);
+  }
+}
+
+// timedelta decode, NaT pass 1: the first index whose encoded value is NaT
+// (8-B astypes only) or whose running sum is INT64_MIN, atomicMin'd into *k
+// (initialised to ~0).  Sums are int64 ticks, `dec_swapped` their byte order.
+__global__ __launch_bounds__(MC_BLOCK) void k_td_first_nat(const uint8_t *__restrict__ enc, int enc_dt,
+                                                          const uint8_t *__restrict__ dec, bool dec_swapped,
+                                                          size_t n, unsigned long long *k) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  const bool enc8 = x_itemsize(enc_dt) == 8;
+  unsigned long long first = ~0ull;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i < n && first == ~0ull) {
+      uint64_t sum = reinterpret_cast<const uint64_t *>(dec)[i];
+      if (dec_swapped) sum = __builtin_bswap64(sum);
+      bool hit = (int64_t)sum == NAT;
+      if (enc8) {
+        uint64_t e = reinterpret_cast<const uint64_t *>(enc)[i];
+        if (mc_dt_swapped(enc_dt)) e = __builtin_bswap64(e);
+        hit = hit || (int64_t)e == NAT;
+      }
+      if (hit) first = i;
+    }
+  }
+  // wave minimum, then one atomic per wave that found something
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(first, off);
+    first = o < first ? o : first;
+  }
+  if ((threadIdx.x & 63) == 0 && first != ~0ull) atomicMin(k, first);
+}
+
+// NaT pass 2: every sum from index *k on is NaT
+__global__ __launch_bounds__(MC_BLOCK) void k_td_fill_nat(uint8_t *__restrict__ dec, size_t n,
+                                                         const unsigned long long *k) {
+  const unsigned long long first = *k;
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  if (first >= n || base + (size_t)(X_STEPS - 1) * MC_BLOCK < first) return;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    // INT64_MIN's bytes are 00..00 80: reversed, 80 00..00 (same bits pattern
+    // read either way apart from the position of 0x80)
+    if (i < n && i >= first) reinterpret_cast<uint64_t *>(dec)[i] = 0x8000000000000000ull;
+  }
+}
+__global__ __launch_bounds__(MC_BLOCK) void k_td_fill_nat_be(uint8_t *__restrict__ dec, size_t n,
+                                                            const unsigned long long *k) {
+  const unsigned long long first = *k;
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  if (first >= n || base + (size_t)(X_STEPS - 1) * MC_BLOCK < first) return;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i < n && i >= first) reinterpret_cast<uint64_t *>(dec)[i] = 0x80ull;
+  }
+}
+
+// byte reversal of n elements of es bytes (a cast that only changes byte
+// order: the bits are never converted, so signalling NaNs stay signalling,
+// as numpy's byte-swapping cast keeps them)
+template <int ES>
+__global__ __launch_bounds__(MC_BLOCK) void k_bswap(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                   size_t nbytes, bool vec) {
+  const size_t base = (size_t)blockIdx.x * (16 * X_STEPS * MC_BLOCK);
+  if (vec) {
+#pragma unroll
+    for (int s = 0; s < X_STEPS; ++s) {
+      const size_t o = base + ((size_t)s * MC_BLOCK + threadIdx.x) * 16;
+      if (o + 16 <= nbytes) {
+        mc_st16<true>(dst + o, mc_bswap_vec<ES>(mc_ld16<true>(src + o)));
+      } else if (o < nbytes) {
+        for (size_t e = o; e + ES <= nbytes; e += ES)
+          mc_store_elem(dst + e, 0, ES, mc_bswap_n(mc_load_elem(src + e, 0, ES), ES));
+      }
+    }
+  } else {
+    for (size_t e = base + (size_t)threadIdx.x * ES; e + ES <= nbytes && e < base + 16 * X_STEPS * MC_BLOCK;
+         e += (size_t)MC_BLOCK * ES)
+      mc_store_elem_u(dst + e, 0, ES, mc_bswap_n(mc_load_elem_u(src + e, 0, ES), ES));
+  }
+}
+
+unsigned x_grid(size_t n) { return (unsigned)((n + (size_t)X_STEPS * MC_BLOCK - 1) / ((size_t)X_STEPS * MC_BLOCK)); }
+
+bool x_aligned(const void *p, int dt) {
+  const int cs = x_is_complex(dt) ? mc_itemsize(x_comp(dt)) : x_itemsize(dt);
+  return (uintptr_t)p % (uintptr_t)cs == 0;
+}
+
+McX x_scalar(int dt, double re, double im, int64_t i) {
+  McX r;
+  if (mc_is_float(dt) || x_is_complex(dt)) {
+    r.re.f = re;
+    r.re.i = 0;
+    r.im = x_is_complex(dt) ? im : 0.0;
+  } else {
+    r.re.f = 0.0;
+    r.re.i = i;
+    r.im = 0.0;
+  }
+  return r;
+}
+
+size_t x_align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// the component dtype of promote_types(astype, dtype) for a complex pair:
+// the wider of the two sides' needs (numpy: i1/u1/b1 fit f2, i2/u2 f4,
+// wider integers f8; complex at least f4)
+int x_promote_comp(int astype, int dtype) {
+  auto need = [](int dt) {
+    switch (mc_dt_base(dt)) {
+      case MC_C8: case MC_F4: case MC_I2: case MC_U2: return 4;
+      case MC_C16: case MC_F8: case MC_I4: case MC_U4: case MC_I8: case MC_U8: return 8;
+      default: return 2;  // b1, i1, u1, f2
+    }
+  };
+  const int w = need(astype) > need(dtype) ? need(astype) : need(dtype);
+  return w == 8 ? MC_F8 : MC_F4;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C++-linkage hooks the real entry points route extended codes to
+// ---------------------------------------------------------------------------
+bool mc_ext_code(int dt) { return x_valid(dt) && x_is_ext(dt); }
+
+int mc_ext_bswap(const void *src, void *dst, size_t n, int es, hipStream_t st) {
+  if (n == 0) return MC_OK;
+  const size_t nbytes = n * (size_t)es;
+  const bool vec = (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
+  const unsigned g = (unsigned)((nbytes + 16 * X_STEPS * MC_BLOCK - 1) / (16 * X_STEPS * MC_BLOCK));
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  switch (es) {
+    case 2: k_bswap<2><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
+    case 4: k_bswap<4><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
+    case 8: k_bswap<8><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
+    default: return MC_EINVAL;
+  }
+  return mc_last_launch();
+}
+
+int mc_ext_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype, hipStream_t st) {
+  if (!x_valid(dtype) || !x_valid(astype)) return MC_EINVAL;
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  k_xdelta_enc<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), n,
+                                                dtype, astype, x_aligned(src, dtype) && x_aligned(dst, astype));
+  return mc_last_launch();
+}
+
+extern "C" int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
+                               size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream);
+extern "C" size_t mc_delta_decode_workspace(size_t n, int astype, int dtype);
+
+// workspace layout of an extended decode (0 = pair not supported)
+static bool td_pair(int astype, int dtype) {
+  const int a = mc_dt_base(astype), d = mc_dt_base(dtype);
+  if (d == MC_TD8) return a == MC_TD8 || (!x_is_ext(a) && !mc_is_float(a));
+  if (d == MC_I8) return a == MC_TD8;
+  return false;
+}
+static bool cx_pair(int astype, int dtype) {
+  if (!x_is_complex(astype) && !x_is_complex(dtype)) return false;
+  return !x_is_time(astype) && !x_is_time(dtype);
+}
+
+static int nanfix(const uint8_t *in, int ac, uint8_t *out, int lc, size_t n, long long *last, long long *carry,
+                  hipStream_t st) {
+  const size_t nb = (n + NF_BLOCK - 1) / NF_BLOCK;
+  if (mc_is_float(ac) == false) return MC_OK;  // integer / bool inputs are never NaN
+  k_nanfix_last<<<(unsigned)nb, MC_BLOCK, 0, st>>>(in, ac, n, last);
+  k_nanfix_scan<<<1, MC_BLOCK, 0, st>>>(last, carry, nb);
+  k_nanfix_apply<<<(unsigned)nb, MC_BLOCK, 0, st>>>(in, ac, out, lc, n, last, carry);
+  return mc_last_launch();
+}
+
+size_t mc_ext_delta_decode_workspace(size_t n, int astype, int dtype) {
+  if (td_pair(astype, dtype)) {
+    const int ia = mc_dt_base(astype) == MC_TD8 ? (MC_I8 | (astype & MC_BIG_ENDIAN)) : astype;
+    const int id = MC_I8 | (dtype & MC_BIG_ENDIAN);
+    return x_align_up(8) + mc_delta_decode_workspace(n, ia, id);
+  }
+  if (cx_pair(astype, dtype)) {
+    const int lc = x_promote_comp(astype, dtype);
+    const int ac = x_is_complex(astype) ? mc_dt_base(x_comp(astype)) : mc_dt_base(astype);
+    const size_t in_planes = x_is_complex(astype) ? 2 * x_align_up(n * mc_itemsize(ac)) : 0;
+    const size_t out_planes = 2 * x_align_up(n * mc_itemsize(lc));
+    const size_t nf = 2 * ((n + NF_BLOCK - 1) / NF_BLOCK) * sizeof(long long);  // NaN-fix blocks
+    const size_t rw = mc_delta_decode_workspace(n, ac, lc);
+    return in_planes + out_planes + (rw > nf ? rw : nf);
+  }
+  return 0;
+}
+
+int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
+                        size_t workspace_bytes, uint32_t *ticket, hipStream_t st) {
+  if (!x_valid(dtype) || !x_valid(astype)) return MC_EINVAL;
+  const bool td = td_pair(astype, dtype), cx = cx_pair(astype, dtype);
+  if (!td && !cx) return MC_EINVAL;
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  const size_t need = mc_ext_delta_decode_workspace(n, astype, dtype);
+  if (!workspace || workspace_bytes < need || (uintptr_t)workspace % 256) return MC_ENOSPC;
+  uint8_t *ws = static_cast<uint8_t *>(workspace);
+  if (td) {
+    // the int64 wrap-around prefix sums (the integer scan), then NaT from the
+    // first NaT operand / INT64_MIN sum on (TIMEDELTA_mm_m_add's NaT rule)
+    const int ia = mc_dt_base(astype) == MC_TD8 ? (MC_I8 | (astype & MC_BIG_ENDIAN)) : astype;
+    const int id = MC_I8 | (dtype & MC_BIG_ENDIAN);
+    if ((uintptr_t)dst % 8 || (x_itemsize(ia) == 8 && (uintptr_t)src % 8)) return MC_EINVAL;
+    unsigned long long *k = reinterpret_cast<unsigned long long *>(ws);
+    int rc = mc_hip_status(hipMemsetAsync(k, 0xFF, 8, st));
+    if (rc) return rc;
+    rc = mc_delta_decode(src, dst, n, ia, id, ws + x_align_up(8), workspace_bytes - x_align_up(8), ticket, st);
+    if (rc) return rc;
+    k_td_first_nat<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), ia,
+                                                   static_cast<const uint8_t *>(dst), mc_dt_swapped(id), n, k);
+    if (mc_dt_swapped(id)) k_td_fill_nat_be<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<uint8_t *>(dst), n, k);
+    else k_td_fill_nat<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<uint8_t *>(dst), n, k);
+    return mc_last_launch();
+  }
+  // complex: per component, the running sums in the loop's component type lc
+  const int lc = x_promote_comp(astype, dtype);
+  const int ac = x_is_complex(astype) ? mc_dt_base(x_comp(astype)) : astype;
+  const size_t lcs = mc_itemsize(lc);
+  size_t off = 0;
+  const uint8_t *in_re = static_cast<const uint8_t *>(src), *in_im = nullptr;
+  if (x_is_complex(astype)) {
+    uint8_t *pre = ws + off, *pim = ws + off + x_align_up(n * mc_itemsize(ac));
+    off += 2 * x_align_up(n * mc_itemsize(ac));
+    k_xsplit<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), pre, pim, n, astype,
+                                             x_aligned(src, astype));
+    int rc = mc_last_launch();
+    if (rc) return rc;
+    in_re = pre;
+    in_im = pim;
+  }
+  uint8_t *out_re = ws + off, *out_im = ws + off + x_align_up(n * lcs);
+  off += 2 * x_align_up(n * lcs);
+  uint8_t *rws = ws + off;
+  const size_t rws_bytes = workspace_bytes - off;
+  // numpy's NaN + NaN operand choice of the complex loop (see k_nanfix_*)
+  const bool second = (lc == MC_F4) != (n == 2);
+  const size_t nb = (n + NF_BLOCK - 1) / NF_BLOCK;
+  long long *nf_last = reinterpret_cast<long long *>(rws), *nf_carry = nf_last + nb;
+  int rc = mc_delta_decode(in_re, out_re, n, ac, lc, rws, rws_bytes, nullptr, st);
+  if (!rc && second) rc = nanfix(in_re, ac, out_re, lc, n, nf_last, nf_carry, st);
+  if (rc) return rc;
+  if (in_im) {
+    rc = mc_delta_decode(in_im, out_im, n, ac, lc, rws, rws_bytes, nullptr, st);
+    if (!rc && second) rc = nanfix(in_im, ac, out_im, lc, n, nf_last, nf_carry, st);
+    if (rc) return rc;
+  }
+  k_xmerge<<<x_grid(n), MC_BLOCK, 0, st>>>(out_re, in_im ? out_im : nullptr, static_cast<uint8_t *>(dst), n, lc,
+                                           dtype, x_aligned(dst, dtype));
+  return mc_last_launch();
+}
+
+static int mc_ext_map(int kind, const void *src, void *dst, size_t n, int d, int t1, int t2, int a, McX s0, McX s1,
+               int64_t num, int64_t den, hipStream_t st) {
+  if (!x_valid(d) || !x_valid(a) || !x_valid(t1) || !x_valid(t2)) return MC_EINVAL;
+  if (mc_dt_swapped(t1) || mc_dt_swapped(t2)) return MC_EINVAL;
+  if (num <= 0 || den <= 0) return MC_EINVAL;
+  if (n == 0) return MC_OK;
+  if (!src || !dst) return MC_EINVAL;
+  XParams p;
+  p.d = d;
+  p.t1 = t1;
+  p.t2 = t2;
+  p.a = a;
+  p.s0 = s0;
+  p.s1 = s1;
+  p.num = num;
+  p.den = den;
+  p.al = x_aligned(src, d) && x_aligned(dst, a);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  uint8_t *o = static_cast<uint8_t *>(dst);
+  switch (kind) {
+    case X_CAST: k_xmap<X_CAST><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
+    case X_FSO_ENC: k_xmap<X_FSO_ENC><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
+    default: k_xmap<X_FSO_DEC><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
+  }
+  return mc_last_launch();
+}
+
+extern "C" {
+
+int mc_cast_units(const void *src, void *dst, size_t n, int from_dtype, int to_dtype, int64_t num, int64_t den,
+                  mc_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!x_valid(from_dtype) || !x_valid(to_dtype)) return MC_EINVAL;
+  if ((num != 1 || den != 1) && !(x_is_time(from_dtype) && x_is_time(to_dtype))) return MC_EINVAL;
+  const int fb = mc_dt_base(from_dtype), tb = mc_dt_base(to_dtype);
+  // same dtype up to byte order (and, for time dtypes, no unit change):
+  // bits moved, never converted
+  const bool same = fb == tb || (x_is_time(fb) && x_is_time(tb));
+  if (same && num == 1 && den == 1) {
+    if (n == 0) return MC_OK;
+    if (!src || !dst) return MC_EINVAL;
+    const int es = x_is_complex(fb) ? mc_itemsize(x_comp(fb)) : x_itemsize(fb);
+    const size_t ne = x_is_complex(fb) ? 2 * n : n;
+    if (mc_dt_swapped(from_dtype) == mc_dt_swapped(to_dtype) || es == 1)
+      return mc_copy_rows_impl(src, ne * es, dst, ne * es, ne * es, 1, st);
+    return mc_ext_bswap(src, dst, ne, es, st);
+  }
+  if (!x_is_ext(from_dtype) && !x_is_ext(to_dtype)) return mc_cast(src, dst, n, from_dtype, to_dtype, stream);
+  const McX z = x_make(mc_num_i(0));
+  return mc_ext_map(X_CAST, src, dst, n, from_dtype, mc_dt_base(from_dtype), mc_dt_base(from_dtype), to_dtype, z,
+                    z, num, den, st);
+}
+
+int mc_fso_encode_x(const void *src, void *dst, size_t n, int dtype, int t1, int t2, int astype, double offset_re,
+                    double offset_im, int64_t offset_i, double scale_re, double scale_im, int64_t scale_i,
+                    mc_stream_t stream) {
+  if (x_is_time(t1) || x_is_time(t2)) return MC_EINVAL;  // numpy has no rint loop for them
+  return mc_ext_map(X_FSO_ENC, src, dst, n, dtype, t1, t2, astype, x_scalar(t1, offset_re, offset_im, offset_i),
+                    x_scalar(t2, scale_re, scale_im, scale_i), 1, 1, (hipStream_t)stream);
+}
+
+int mc_fso_decode_x(const void *src, void *dst, size_t n, int astype, int t3, int t4, int dtype, double scale_re,
+                    double scale_im, double offset_re, double offset_im, mc_stream_t stream) {
+  if (!(mc_is_float(t3) || x_is_complex(t3)) || !(mc_is_float(t4) || x_is_complex(t4))) return MC_EINVAL;
+  return mc_ext_map(X_FSO_DEC, src, dst, n, astype, t3, t4, dtype, x_scalar(t3, scale_re, scale_im, 0),
+                    x_scalar(t4, offset_re, offset_im, 0), 1, 1, (hipStream_t)stream);
+}
+
+}  // extern "C"

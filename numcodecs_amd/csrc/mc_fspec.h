@@ -76,7 +76,10 @@ struct FsT {
   MC_DEV static S bound(double pre, double sum) { return round((P)pre + (P)sum); }
   MC_DEV static V val(S c) { return (V)c; }
   MC_DEV static S store(V r) { return (S)r; }  // exact: r holds a D value
+  // numpy's recurrence value (exact, x86 NaN choice: it may be stored) /
+  // the same for a bitwise check that treats non-finite values as failures
   MC_DEV static V step(V pv, V x) { return ser_add<D>(pv, x); }
+  MC_DEV static V step_raw(V pv, V x) { return ser_add_raw<D>(pv, x); }
   MC_DEV static uint64_t bits(S c) {
     if constexpr (sizeof(S) == 8) return __builtin_bit_cast(uint64_t, c);
     else if constexpr (sizeof(S) == 4) return __builtin_bit_cast(uint32_t, c);
@@ -316,7 +319,7 @@ MC_DEV uint64_t fs_check(const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W],
     for (int e = W - 1; e >= 0; --e) {
       const size_t g = e0 + e;
       const typename Tr::S pv = e ? c[q][e - 1] : p0[q];
-      const typename Tr::S r = g == 0 ? Tr::store(v[q][0]) : Tr::store(Tr::step(Tr::val(pv), v[q][e]));
+      const typename Tr::S r = g == 0 ? Tr::store(v[q][0]) : Tr::store(Tr::step_raw(Tr::val(pv), v[q][e]));
       // a non-finite input makes its own prefix (and so c) non-finite
       const bool ok = Tr::bits(c[q][e]) == Tr::bits(r) && Tr::finite(c[q][e]);
       if (g < n && !ok) first = g;
@@ -541,11 +544,11 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
     for (; j + 2 * FSW_G <= cnt; j += 2 * FSW_G) {
       ser_ld<T, FSW_G>(p + j + FSW_G, gb);
       __builtin_amdgcn_sched_barrier(0);
-      acc = ser_group<D, FSW_G>(acc, ga);
+      acc = ser_group<D, FSW_G>(acc, ga, p + j);
       ser_st<T, FSW_G>(o + j, ga);
       ser_ld<T, FSW_G>(p + j + 2 * FSW_G, ga);
       __builtin_amdgcn_sched_barrier(0);
-      acc = ser_group<D, FSW_G>(acc, gb);
+      acc = ser_group<D, FSW_G>(acc, gb, p + j + FSW_G);
       ser_st<T, FSW_G>(o + j + FSW_G, gb);
     }
   }
@@ -973,7 +976,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           for (int e = 0; e < W; ++e) {
             const int li = fsw_li(q, e, W);
             const S pe = e ? c[q][e - 1] : pvs[q];
-            const S r = Tr::store(Tr::step(Tr::val(pe), v[q][e]));
+            const S r = Tr::store(Tr::step_raw(Tr::val(pe), v[q][e]));
             // non-short-circuit (&): no control flow per element
             const bool ok = (Tr::bits(c[q][e]) == Tr::bits(r)) & Tr::finite(c[q][e]);
             const bool bad = (!ok) & (li > fpos) & (li < cnt) & !(q == 0 && e == 0 && lane == 0);

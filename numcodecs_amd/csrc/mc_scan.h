@@ -195,34 +195,51 @@ static inline void mc_launch_scan_sums_mw(const uint64_t *in, uint64_t *out, siz
 template <int D> struct SerAcc { using T = float; };
 template <> struct SerAcc<MC_F8> { using T = double; };
 
+// numpy's add of the running sum a and the next value b: IEEE add in D's
+// loop type with x86-64's NaN choice (mc_x86_nan: a's NaN quieted, else b's,
+// else the negative default NaN) -- the GPU's own NaN results differ (NaN +
+// NaN keeps the second operand here, inf + -inf is +NaN).  f2: numpy's half
+// loop, float32 add then npy_float_to_half (the hardware RNE conversion, with
+// denormals kept, gives the same half for every non-NaN sum; NaN sums take
+// numpy's payload-preserving routine).
 template <int D>
 MC_DEV typename SerAcc<D>::T ser_add(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
   if constexpr (D == MC_F2) {
-    // numpy's half loop: float32 add, then npy_float_to_half.  The hardware
-    // RNE conversion (denormals kept) gives the same half for every non-NaN
-    // sum; NaN sums take numpy's payload-preserving routine.
+    // numpy's half loop keeps the SECOND operand's NaN when both are NaN
+    // (measured: cumsum of [NaN_a, NaN_b] gives NaN_b for float16; float32 /
+    // float64 keep the first)
     const float r = a + b;
-    if (__builtin_isnan(r)) return mc_half_to_float(mc_float_to_half(r));
+    if (__builtin_isnan(r)) return mc_half_to_float(mc_float_to_half(mc_x86_nan(b, a, r)));
     return (float)(_Float16)r;
   } else {
-    return a + b;
+    const typename SerAcc<D>::T r = a + b;
+    return __builtin_isnan(r) ? mc_x86_nan(a, b, r) : r;
   }
+}
+// the same sum where a NaN result is only tested, never stored (the
+// speculative verification counts non-finite candidates as failures)
+template <int D>
+MC_DEV typename SerAcc<D>::T ser_add_raw(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
+  if constexpr (D == MC_F2) return ser_add<D>(a, b);
+  else return a + b;
 }
 
 // One group of the chain, in place (g[k] <- the running sum after g[k]).
 // f2: numpy adds in float32 and rounds to half; with float32's 24 >= 2*11+2
 // bits that double rounding equals one correctly rounded half add, so the
 // group runs as a chain of half adds (v_add_f16, one dependent op per
-// element; LLVM folds the float<->half round trips between them).  NaN is
-// absorbing in the chain, so a group ending in NaN is recomputed with the
-// exact routine (ser_add: numpy's payload-preserving conversion, x86's NaN
-// choice) from its first value -- the GPU's own NaN results differ (inf +
-// -inf is +NaN here, -NaN on x86).
+// element; LLVM folds the float<->half round trips between them).  f4 / f8:
+// plain dependent adds.  NaN is absorbing in the chain, so a group ending in
+// NaN is recomputed with the exact routine (ser_add: numpy's payload-
+// preserving conversion, x86's NaN choice) from its first value; `src`
+// holds the group's inputs (the LDS slot the group was read from, not yet
+// overwritten) for the f4 / f8 recompute, whose in-place registers hold sums.
 template <int D, int G>
-MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAcc<D>::T (&g)[G]) {
+MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAcc<D>::T (&g)[G],
+                                       const typename SerAcc<D>::T *src) {
   using T = typename SerAcc<D>::T;
+  const T a0 = acc;
   if constexpr (D == MC_F2) {
-    const T a0 = acc;
     T r[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
@@ -242,8 +259,15 @@ MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAc
   } else {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      acc = ser_add<D>(acc, g[k]);
+      acc = acc + g[k];
       g[k] = acc;
+    }
+    if (__builtin_isnan(acc)) {
+      acc = a0;
+      for (int k = 0; k < G; ++k) {
+        acc = ser_add<D>(acc, src[k]);
+        g[k] = acc;
+      }
     }
   }
   return acc;

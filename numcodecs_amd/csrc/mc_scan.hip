@@ -713,6 +713,28 @@ static void launch_fspec_rows_any(const uint8_t *sc, size_t ss, uint8_t *dc, siz
   }
 }
 
+// np.cumsum's first output is its first input cast to dtype; with the same
+// float type up to byte order that cast moves bits, so a signalling NaN there
+// keeps its payload.  The decode kernels compute element 0 through a value
+// conversion (which quiets it) where the byte order changes or the type is
+// f2: this one-thread-per-row pass re-writes it with the input's bits.
+__global__ void k_first_elem_bits(const uint8_t *__restrict__ src, size_t ss, uint8_t *__restrict__ dst,
+                                  size_t ds, size_t rows, int es, bool swap) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  uint64_t v = mc_load_elem_u(src + r * ss, 0, es);
+  if (swap) v = mc_bswap_n(v, es);
+  mc_store_elem_u(dst + r * ds, 0, es, v);
+}
+
+static void fix_first_elems(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t rows, int astype,
+                            int dtype, hipStream_t st) {
+  if (!mc_is_float(dtype) || mc_dt_base(astype) != mc_dt_base(dtype) || rows == 0) return;
+  const bool swap = mc_dt_swapped(astype) != mc_dt_swapped(dtype);
+  if (!swap && mc_dt_base(dtype) != MC_F2) return;
+  k_first_elem_bits<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(s, ss, d, ds, rows, mc_itemsize(dtype), swap);
+}
+
 }  // namespace
 
 int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, size_t dst_stride,
@@ -722,6 +744,7 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
 extern "C" {
 
 size_t mc_delta_decode_workspace(size_t n, int astype, int dtype) {
+  if (mc_ext_code(astype) || mc_ext_code(dtype)) return mc_ext_delta_decode_workspace(n, astype, dtype);
   if (mc_is_float(dtype)) return fspec_types_ok(astype, dtype) ? fspec_ws_bytes(n, dtype) : 0;
   const size_t generic = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE * sizeof(uint64_t);
   if (astype != dtype || dtype == MC_B1) return generic;
@@ -747,6 +770,8 @@ static bool delta_decode_pair_ok(int astype, int dtype) {
 int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
                     size_t workspace_bytes, uint32_t *ticket, mc_stream_t stream) {
   if (ticket && (uintptr_t)ticket % 8) return MC_EINVAL;
+  if (mc_ext_code(astype) || mc_ext_code(dtype))
+    return mc_ext_delta_decode(src, dst, n, astype, dtype, workspace, workspace_bytes, ticket, (hipStream_t)stream);
   if (!mc_valid_dtype(dtype) || !mc_valid_dtype(astype)) return MC_EINVAL;
   if (!delta_decode_pair_ok(astype, dtype)) return MC_EINVAL;
   if (n == 0) return MC_OK;
@@ -762,9 +787,11 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
         workspace_bytes >= fspec_ws_bytes(n, dtype) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
         (uintptr_t)workspace % 8 == 0) {
       launch_fspec_any(s, d, n, astype, dtype, workspace, st);
+      fix_first_elems(s, 0, d, 0, 1, astype, dtype, st);
       return mc_last_launch();
     }
     mc_launch_serial_any(s, 0, d, 0, n, 1, astype, dtype, st);
+    fix_first_elems(s, 0, d, 0, 1, astype, dtype, st);
     return mc_last_launch();
   }
   const size_t ntiles = (n + MC_SCAN_TILE - 1) / MC_SCAN_TILE;
@@ -839,6 +866,7 @@ int mc_delta_decode_batch_ws(const void *src, size_t src_stride, void *dst, size
     const uint8_t *sc = s + c0 * src_stride;
     uint8_t *dc = d + c0 * dst_stride;
     launch_fspec_rows_any(sc, src_stride, dc, dst_stride, n, astype, dtype, fail + c0, g, st);
+    fix_first_elems(sc, src_stride, dc, dst_stride, g, astype, dtype, st);
   }
   return mc_last_launch();
 }
@@ -868,6 +896,7 @@ int mc_delta_decode_batch_impl(const void *src, size_t src_stride, void *dst, si
     uint8_t *dc = d + c0 * dst_stride;
     if (mc_is_float(dtype)) {
       mc_launch_serial_any(sc, src_stride, dc, dst_stride, n, rows, astype, dtype, st, variant);
+      fix_first_elems(sc, src_stride, dc, dst_stride, rows, astype, dtype, st);
       continue;
     }
     const size_t as = mc_itemsize(astype), ds = mc_itemsize(dtype);

@@ -155,11 +155,11 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
         for (; j + 2 * SER_G <= cnt; j += 2 * SER_G) {
           ser_ld<T, SER_G>(p + j + SER_G, gb);
           __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead ahead of the adds
-          acc = ser_group<L, SER_G>(acc, ga);
+          acc = ser_group<L, SER_G>(acc, ga, p + j);
           ser_st<T, SER_G>(o + j, ga);
           ser_ld<T, SER_G>(p + j + 2 * SER_G, ga);
           __builtin_amdgcn_sched_barrier(0);
-          acc = ser_group<L, SER_G>(acc, gb);
+          acc = ser_group<L, SER_G>(acc, gb, p + j + SER_G);
           ser_st<T, SER_G>(o + j + SER_G, gb);
         }
       }

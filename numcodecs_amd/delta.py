@@ -50,6 +50,66 @@ def decode_loop_dtype(astype, dtype):
     return None
 
 
+def _dry_run_encode(dtype, astype):
+    """delta.py:65-66 on a two-element stand-in: numpy's own errors and
+    warnings (e.g. ComplexWarning) for the differences of an extended-dtype
+    pair.  The first element's assignment (delta.py:63) depends on its value
+    (a timedelta64 scalar may convert through datetime.timedelta): it is
+    replayed with the real value by check_first_elements."""
+    arr = np.zeros(2, dtype=dtype)
+    enc = np.empty_like(arr, dtype=astype)
+    enc[1:] = np.diff(arr)
+
+
+def _dry_run_decode(astype, dtype):
+    """delta.py:77-80 on a stand-in: np.cumsum raises numpy's UFuncTypeError
+    for a datetime64 dtype (no datetime + datetime loop) or a float astype
+    into timedelta64, exactly as the reference does."""
+    np.cumsum(np.zeros(2, dtype=astype), out=np.empty(2, dtype=dtype))
+
+
+def ext_delta_encode(src, dst, n, dtype, astype) -> None:
+    """Delta encode with a complex / timedelta64 / datetime64 side: the
+    differences in dtype (mc_ext.hip), cast to astype; a timedelta astype of
+    another unit through numpy's unit cast (mc_cast_units)."""
+    _dry_run_encode(dtype, astype)
+    d, a = np.dtype(dtype), np.dtype(astype)
+    if d.kind in "mM" and a.kind in "mM" and np.datetime_data(a) != np.datetime_data(d):
+        if d.kind == "M" or a.kind == "M":
+            # numpy converts the first element (a datetime scalar) and the
+            # differences (timedeltas) with different cast rules here
+            raise NotImplementedError(
+                f"Delta({d.str!r}, astype={a.str!r}): datetime64 with a unit change is not supported by the "
+                "numcodecs_amd device kernels")
+        tmp = torch.empty(n * 8, dtype=torch.uint8, device=src.device)
+        _ops.delta_encode(src, tmp, n, d, d)  # timedelta differences in dtype's unit
+        _ops.cast(tmp, dst, n, d, a)
+        return
+    _ops.delta_encode(src, dst, n, d, a)
+
+
+def ext_delta_decode(src, dst, n, astype, dtype) -> None:
+    """Delta decode with a complex / timedelta64 side (mc_ext.hip): numpy's
+    timedelta running sums (NaT from the first NaT on) or per-component
+    complex running sums.  An astype numpy converts first (another timedelta
+    unit) goes through mc_cast_units; an integer dtype from a timedelta
+    astype is decoded as timedelta and cast, as numpy's loop does."""
+    _dry_run_decode(astype, dtype)
+    a, d = np.dtype(astype), np.dtype(dtype)
+    if d.kind == "m" and a.kind == "m" and np.datetime_data(a) != np.datetime_data(d):
+        tmp = torch.empty(n * 8, dtype=torch.uint8, device=src.device)
+        _ops.cast(src, tmp, n, a, d)
+        _ops.delta_decode(tmp, dst, n, d, d)
+        return
+    if a.kind == "m" and d.kind != "m" and not (d.kind == "i" and d.itemsize == 8):
+        loop = a.newbyteorder("=")
+        tmp = torch.empty(n * 8, dtype=torch.uint8, device=src.device)
+        _ops.delta_decode(src, tmp, n, a, loop)
+        _ops.cast(tmp, dst, n, loop, d)
+        return
+    _ops.delta_decode(src, dst, n, a, d)
+
+
 def decode_two_step(src, dst, n, astype, dtype, loop) -> None:
     """Delta decode of a pair decode_loop_dtype() routes through its loop
     dtype: running sums into a device temporary of `loop`, then cast."""
@@ -89,7 +149,10 @@ class Delta(Codec):
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")
         check_first_elements(src.data[: self.dtype.itemsize], self.dtype, self.astype)
         dst = empty_like_bytes(n * self.astype.itemsize, src)
-        _ops.delta_encode(src.data, dst, n, self.dtype, self.astype)
+        if _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype):
+            ext_delta_encode(src.data, dst, n, self.dtype, self.astype)
+        else:
+            _ops.delta_encode(src.data, dst, n, self.dtype, self.astype)
         return finish(dst, self.astype, (n,), "C", src.host)
 
     def decode(self, buf, out=None):
@@ -97,10 +160,13 @@ class Delta(Codec):
         if src.nbytes % self.astype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.astype.itemsize
-        loop = decode_loop_dtype(self.astype, self.dtype)
+        ext = _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype)
+        loop = None if ext else decode_loop_dtype(self.astype, self.dtype)
         direct = device_out_bytes(out, n * self.dtype.itemsize, src)
         dst = empty_like_bytes(n * self.dtype.itemsize, src) if direct is None else direct
-        if loop is None:
+        if ext:
+            ext_delta_decode(src.data, dst, n, self.astype, self.dtype)
+        elif loop is None:
             _ops.delta_decode(src.data, dst, n, self.astype, self.dtype)
         elif n:
             decode_two_step(src.data, dst, n, self.astype, self.dtype, loop)

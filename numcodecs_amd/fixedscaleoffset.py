@@ -55,6 +55,11 @@ class FixedScaleOffset(Codec):
         if src.nbytes % self.dtype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.dtype.itemsize
+        if _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype):
+            # the reference's expression on a stand-in: numpy's own errors
+            # (no rint loop for timedelta64, no multiply for datetime64) and
+            # warnings (ComplexWarning on a complex -> real astype)
+            np.around((np.zeros(1, dtype=self.dtype) - self.offset) * self.scale).astype(self.astype, copy=False)
         t1, off = _resolve(np.subtract, self.dtype, self.offset)
         t2, sc = _resolve(np.multiply, t1, self.scale)
         dst = empty_like_bytes(n * self.astype.itemsize, src)
@@ -66,6 +71,8 @@ class FixedScaleOffset(Codec):
         if src.nbytes % self.astype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.astype.itemsize
+        if _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype):
+            ((np.zeros(1, dtype=self.astype) / self.scale) + self.offset).astype(self.dtype, copy=False)
         t3, sc = _resolve(np.true_divide, self.astype, self.scale)
         t4, off = _resolve(np.add, t3, self.offset)
         direct = device_out_bytes(out, n * self.dtype.itemsize, src)

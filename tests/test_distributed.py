@@ -84,7 +84,8 @@ def test_bench_self_launches_ranks_dry_run(world):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run"],
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--dry-run",
+                        "--cpu-seconds", "0.2", "--cpu-procs", "2"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -105,6 +106,32 @@ def test_bench_self_launches_ranks_dry_run(world):
     # per-rank GPU-event times exist in the record (none on a CPU rehearsal)
     assert all("gpu_event_s" in x for x in d["ranks"])
     assert d["event_aggregate_GiBps"] is None and "host_minus_event_s" in d
+    # the CPU baseline survives N > 1: timed by the launcher parent before
+    # the ranks start, handed to rank 0
+    cb = d["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] == "port"
+    assert cb["parallel_cores"] == 2 and cb["parallel_value"] > 0
+
+
+def test_bench_torchrun_rank0_times_cpu_baseline():
+    """Under torch.distributed.run (WORLD_SIZE set, no launcher file) rank 0
+    times the CPU legs itself before joining the process group."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--cpu-seconds", "0.2",
+                        "--cpu-procs", "2"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_ranks"] == 2 and d["cpu_baseline"] is not None and d["cpu_baseline"]["cores"] == 1
 
 
 def test_scaling_fields_physical_gpus():

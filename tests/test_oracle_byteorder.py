@@ -84,7 +84,8 @@ def test_dtype_codes_carry_the_byte_order_flag():
         assert dtype_code(">" + s) == dtype_code("<" + s) | 32
     for s in ("i1", "u1", "b1"):  # numpy has no byte order for 1-byte types
         assert dtype_code(">" + s) == dtype_code("<" + s) == dtype_code("|" + s)
+    assert dtype_code(">c8") == dtype_code("<c8") | 32  # extended dtypes (round 5)
     with pytest.raises(NotImplementedError):
-        dtype_code("<c8")
+        dtype_code("|S4")
     with open(os.path.join(os.path.dirname(GOLDEN), "..", "include", "mcodec.h")) as f:
         assert "#define MC_BIG_ENDIAN 32" in f.read()
