@@ -595,7 +595,7 @@ def _fletcher32_unshuffle(sh: Shuffle, x: torch.Tensor) -> torch.Tensor:
 
 
 def host_pipeline(host_in: torch.Tensor, host_out: torch.Tensor, elementsize: int, encode=True,
-                  slice_chunks: "int | None" = None, nslots: int = 3, device=None) -> None:
+                  slice_chunks: "int | None" = None, nslots: int = 3, device=None, devices=None) -> None:
     """Shuffle a batch of chunks that lives in (pinned) host memory.
 
     The Zarr caller's chunks start and end in host memory (a file or socket

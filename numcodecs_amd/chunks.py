@@ -28,7 +28,7 @@ import math
 
 import torch
 
-from . import _native, batch
+from . import _native, batch, multi
 from .astype import AsType
 from .bitround import BitRound
 from .checksum32 import CRC32, CRC32C, Adler32, JenkinsLookup3
@@ -151,14 +151,20 @@ def _fused_c4_at(codecs, i):
     return i + 3 <= len(codecs) and batch._c4_scalars(*codecs[i:i + 3]) is not None
 
 
-def encode_chunks(codecs, chunks: torch.Tensor) -> torch.Tensor:
+def encode_chunks(codecs, chunks: torch.Tensor, devices=None) -> torch.Tensor:
     """Encode every row of the device batch `chunks` ([B, ...], typed as the
     first codec expects) through `codecs` in order; returns [B, m].  A
-    FixedScaleOffset -> Delta -> Shuffle run encodes in one fused launch."""
+    FixedScaleOffset -> Delta -> Shuffle run encodes in one fused launch.
+    ``devices=[...]`` spreads contiguous row ranges over those GPUs, one
+    worker thread each (numcodecs_amd.multi); the result is gathered in row
+    order on `chunks`' device."""
     if not is_device_tensor(chunks) or chunks.dim() < 1:
         raise TypeError("encode_chunks takes a device tensor [B, ...]")
-    x = chunks.reshape(chunks.shape[0], -1)
     codecs = list(codecs)
+    if devices is not None:
+        y, _ = multi.device_rows(lambda d: (encode_chunks(codecs, d), None), chunks, devices)
+        return y
+    x = chunks.reshape(chunks.shape[0], -1)
     i = 0
     while i < len(codecs):
         if _fused_c4_at(codecs, i):
@@ -172,13 +178,30 @@ def encode_chunks(codecs, chunks: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def decode_chunks(codecs, chunks: torch.Tensor, _pending=None) -> torch.Tensor:
+def decode_chunks(codecs, chunks: torch.Tensor, _pending=None, devices=None) -> torch.Tensor:
     """Invert :func:`encode_chunks` (codecs given in encode order); raises
-    the codec's RuntimeError if any row's checksum does not match."""
+    the codec's RuntimeError if any row's checksum does not match.
+    ``devices=[...]``: as for encode_chunks; the checksum comparisons of all
+    workers are made after they finish, chain step by chain step and row
+    range by row range -- the mismatch the one-device call would raise."""
     if not is_device_tensor(chunks) or chunks.dim() < 1:
         raise TypeError("decode_chunks takes a device tensor [B, ...]")
-    x = chunks.reshape(chunks.shape[0], -1)
     codecs = list(codecs)
+    if devices is not None:
+        def one(d):
+            pend = []
+            return decode_chunks(codecs, d, pend), pend
+
+        y, pends = multi.device_rows(one, chunks, devices)
+        steps = [[p[k] for p in pends] for k in range(len(pends[0]))] if pends and pends[0] else []
+        for step in steps:
+            for c, sums, stored in step:
+                if _pending is None:
+                    _raise_first(c, sums, stored)
+                else:
+                    _pending.append((c, sums, stored))
+        return y
+    x = chunks.reshape(chunks.shape[0], -1)
     i = len(codecs)
     while i > 0:
         if i >= 3 and _fused_c4_at(codecs, i - 3):
@@ -278,12 +301,24 @@ def _host_rows(x, name):
 
 
 def host_encode_chunks(codecs, host_in: torch.Tensor, host_out: "torch.Tensor | None" = None,
-                       slice_chunks: "int | None" = None, nslots: int = 3, device=None) -> torch.Tensor:
+                       slice_chunks: "int | None" = None, nslots: int = 3, device=None,
+                       devices=None) -> torch.Tensor:
     """Encode a batch of host chunks [B, ...] (typed as the first codec
     expects; pin it) through `codecs` on the GPU, streamed; returns the
-    [B, m] uint8 host batch (pinned when allocated here)."""
+    [B, m] uint8 host batch (pinned when allocated here).  ``devices=[...]``
+    streams contiguous row ranges through those GPUs at once, one worker
+    thread and ring each (the host path is PCIe-bound per GPU)."""
     codecs = list(codecs)
     src = _host_rows(host_in, "host_in")
+    if devices is not None:
+        devs = multi.normalize_devices(devices)
+        if host_out is None:
+            probe = encode_chunks(codecs, src[:1].to(devs[0]))
+            host_out = torch.empty((src.shape[0], _rows(probe, 1).shape[1]), dtype=torch.uint8, pin_memory=True)
+        out = _host_rows(host_out, "host_out")
+        multi.host_rows(lambda dev, lo, hi: host_encode_chunks(codecs, src[lo:hi], out[lo:hi], slice_chunks, nslots,
+                                                               dev), src.shape[0], devs)
+        return host_out
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     # encoded row size: run the chain on the first chunk
     probe = encode_chunks(codecs, src[:1].to(device))
@@ -298,13 +333,20 @@ def host_encode_chunks(codecs, host_in: torch.Tensor, host_out: "torch.Tensor | 
 
 
 def host_decode_chunks(codecs, host_in: torch.Tensor, host_out: torch.Tensor,
-                       slice_chunks: "int | None" = None, nslots: int = 3, device=None) -> torch.Tensor:
+                       slice_chunks: "int | None" = None, nslots: int = 3, device=None,
+                       devices=None) -> torch.Tensor:
     """Decode a [B, m] uint8 host batch of encoded chunks through `codecs`
     (given in encode order) into `host_out` ([B, ...] host tensor of the
-    decoded chunks' dtype and size); checksums are verified."""
+    decoded chunks' dtype and size); checksums are verified.  ``devices``:
+    as for host_encode_chunks (a mismatch is raised after every worker
+    finished, the first row range's first)."""
     codecs = list(codecs)
     src = _host_rows(host_in, "host_in")
     out = _host_rows(host_out, "host_out")
+    if devices is not None:
+        multi.host_rows(lambda dev, lo, hi: host_decode_chunks(codecs, src[lo:hi], out[lo:hi], slice_chunks, nslots,
+                                                               dev), src.shape[0], devices)
+        return host_out
     pending = []  # checksum comparisons, checked once after the stream (no per-slice host sync)
 
     def fn(d):

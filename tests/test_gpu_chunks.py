@@ -289,3 +289,66 @@ def test_few_large_rows_decode_row_by_row(device):
     out = batch.delta_chunks(torch.from_numpy(eh2.view(np.uint8)).to(device), d, encode=False).cpu().numpy()
     for i in range(b):
         assert out[i].tobytes() == oracle.delta_decode(eh2[i], "<i4", "<i2").view(np.uint8).tobytes(), i
+
+
+# ---------------------------------------------------------------------------
+# in-process multi-GPU dispatch (numcodecs_amd.multi): devices=[cuda:0,
+# cuda:0] runs two independent workers with their own streams and rings on
+# the one GPU of the box -- the same partition, threads and gathering as a
+# multi-GPU node (unmeasured there)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["bitround_shuffle_crc32", "fso_delta_shuffle_adler32", "delta_shuffle_crc32c",
+                                  "quantize_shuffle_fletcher32"])
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_multi_device_chunks_vs_oracle(device, name, ndev):
+    codecs, dtype = _chains()[name]
+    b = 11
+    devs = [device] * ndev
+    x = _make(dtype, b, 4096 + 64, device, 21)
+    xh = x.cpu().numpy()
+    enc = chunks.encode_chunks(codecs, x, devices=devs)
+    enc_u8 = _rows_u8(enc, b)
+    for i in range(b):
+        assert enc_u8[i].tobytes() == oracle_chain.chain_encode(codecs, xh[i]), (name, i)
+    assert torch.equal(enc.view(torch.uint8).reshape(b, -1), chunks.encode_chunks(codecs, x).view(torch.uint8).reshape(b, -1))
+    dec = chunks.decode_chunks(codecs, enc, devices=devs)
+    dec_u8 = _rows_u8(dec, b)
+    for i in range(b):
+        assert dec_u8[i].tobytes() == oracle_chain.chain_decode(codecs, enc_u8[i].tobytes()), (name, i)
+    # host-streamed, several workers at once
+    host = x.cpu().pin_memory()
+    eh = chunks.host_encode_chunks(codecs, host, slice_chunks=2, devices=devs).numpy()
+    assert eh.tobytes() == enc_u8.tobytes()
+    out = torch.empty_like(host).pin_memory()
+    chunks.host_decode_chunks(codecs, torch.from_numpy(eh).pin_memory(), out, slice_chunks=3, devices=devs)
+    assert out.view(torch.uint8).reshape(b, -1).numpy().tobytes() == dec_u8.tobytes()
+
+
+def test_multi_device_decode_raises_first_mismatch(device):
+    """A corrupted row in the second worker's range raises the reference's
+    RuntimeError after both workers finished."""
+    codecs, dtype = _chains()["bitround_shuffle_crc32"]
+    x = _make(dtype, 8, 4096, device, 22)
+    enc = chunks.encode_chunks(codecs, x, devices=[device, device]).clone()
+    enc.view(torch.uint8)[6, 40] ^= 1
+    with pytest.raises(RuntimeError, match="crc32 checksum do not match"):
+        chunks.decode_chunks(codecs, enc, devices=[device, device])
+    host = enc.cpu().pin_memory()
+    out = torch.empty((8, 4096), dtype=torch.float32).pin_memory()
+    with pytest.raises(RuntimeError, match="crc32 checksum do not match"):
+        chunks.host_decode_chunks(codecs, host, out, slice_chunks=2, devices=[device, device])
+
+
+@pytest.mark.parametrize("es", [4, 8])
+def test_multi_device_host_pipeline_vs_oracle(device, es):
+    b, n = 13, 65536 + 16 * es
+    g = torch.Generator().manual_seed(23)
+    host_in = torch.randint(0, 256, (b, n), generator=g, dtype=torch.uint8).pin_memory()
+    host_out = torch.empty_like(host_in).pin_memory()
+    batch.host_pipeline(host_in, host_out, es, encode=True, slice_chunks=3, devices=[device, device, device])
+    hi, ho = host_in.numpy(), host_out.numpy()
+    for i in range(b):
+        assert ho[i].tobytes() == oracle.shuffle(hi[i], es).tobytes(), i
+    back = torch.empty_like(host_in).pin_memory()
+    batch.host_pipeline(host_out, back, es, encode=False, slice_chunks=2, devices=[device, device])
+    assert torch.equal(back, host_in)
