@@ -76,10 +76,7 @@ struct FsT {
   MC_DEV static S bound(double pre, double sum) { return round((P)pre + (P)sum); }
   MC_DEV static V val(S c) { return (V)c; }
   MC_DEV static S store(V r) { return (S)r; }  // exact: r holds a D value
-  // numpy's recurrence value (exact, x86 NaN choice: it may be stored) /
-  // the same for a bitwise check that treats non-finite values as failures
   MC_DEV static V step(V pv, V x) { return ser_add<D>(pv, x); }
-  MC_DEV static V step_raw(V pv, V x) { return ser_add_raw<D>(pv, x); }
   MC_DEV static uint64_t bits(S c) {
     if constexpr (sizeof(S) == 8) return __builtin_bit_cast(uint64_t, c);
     else if constexpr (sizeof(S) == 4) return __builtin_bit_cast(uint32_t, c);
@@ -319,7 +316,7 @@ MC_DEV uint64_t fs_check(const typename FsT<A_, D>::S (&c)[FS_Q][FsT<A_, D>::W],
     for (int e = W - 1; e >= 0; --e) {
       const size_t g = e0 + e;
       const typename Tr::S pv = e ? c[q][e - 1] : p0[q];
-      const typename Tr::S r = g == 0 ? Tr::store(v[q][0]) : Tr::store(Tr::step_raw(Tr::val(pv), v[q][e]));
+      const typename Tr::S r = g == 0 ? Tr::store(v[q][0]) : Tr::store(Tr::step(Tr::val(pv), v[q][e]));
       // a non-finite input makes its own prefix (and so c) non-finite
       const bool ok = Tr::bits(c[q][e]) == Tr::bits(r) && Tr::finite(c[q][e]);
       if (g < n && !ok) first = g;
@@ -544,11 +541,11 @@ MC_DEV typename SerAcc<D>::T fsw_chain(typename SerAcc<D>::T *p, int j, int cnt,
     for (; j + 2 * FSW_G <= cnt; j += 2 * FSW_G) {
       ser_ld<T, FSW_G>(p + j + FSW_G, gb);
       __builtin_amdgcn_sched_barrier(0);
-      acc = ser_group<D, FSW_G>(acc, ga, p + j);
+      acc = ser_group<D, FSW_G>(acc, ga);
       ser_st<T, FSW_G>(o + j, ga);
       ser_ld<T, FSW_G>(p + j + 2 * FSW_G, ga);
       __builtin_amdgcn_sched_barrier(0);
-      acc = ser_group<D, FSW_G>(acc, gb, p + j + FSW_G);
+      acc = ser_group<D, FSW_G>(acc, gb);
       ser_st<T, FSW_G>(o + j + FSW_G, gb);
     }
   }
@@ -736,7 +733,7 @@ template <int A_, int D, int SW = 0>
 MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_t n, int a, size_t tb, size_t te,
                                          typename FsT<A_, D>::S yin, bool has_in,
                                          typename FsT<A_, D>::V (*xs)[fs_tile_of(D) + 2 * FSW_G],
-                                         typename FsT<A_, D>::S *ldsy) {
+                                         typename FsT<A_, D>::S *ldsy, size_t *nan_at) {
   using Tr = FsT<A_, D>;
   using S = typename Tr::S;
   using V = typename Tr::V;
@@ -828,6 +825,7 @@ MC_DEV typename FsT<A_, D>::S fsw_stream(const uint8_t *src, uint8_t *dst, size_
         }
         if constexpr (DIRECT) acc = fsw_chain<D, true>(p, j, cnt, acc, out);
         else acc = fsw_chain<D>(p, j, cnt, acc);
+        if (D != MC_F2 && *nan_at == SER_NO_NAN && __builtin_isnan(acc)) *nan_at = t0;  // ser_nan_fix
         if (t + 1 == te) *ldsy = Tr::store(acc);
       }
     } else {
@@ -868,6 +866,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
   __shared__ int lds_fi[2][FSW_NW];
   __shared__ uint64_t ldsx[FSW_NW];
   __shared__ S ldsy;
+  __shared__ size_t nan_at;              // first tile whose chain ended NaN (ser_nan_fix)
+  __shared__ unsigned long long nan_k0;
   __shared__ __attribute__((aligned(16))) V xs2[2][TE + 2 * FSW_G];
   V *xs = xs2[0];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -878,6 +878,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
   size_t t = 0;
   bool has_in = false;
   S yin = (S)0;
+  if (threadIdx.x == 0) nan_at = SER_NO_NAN;  // published by the loop's first barrier
   if (single) {
     const uint64_t f = *fail;  // the first index that failed at apply time
     if (f >= n) return;        // everything verified: dst is final
@@ -904,7 +905,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     if (serial_run > 0 && t < next_probe) {
       // noise-like stretch: serial streaming up to the next probe tile
       const size_t te = next_probe < ntiles ? next_probe : ntiles;
-      yin = fsw_stream<A_, D, SW>(src, dst, n, a, t, te, yin, has_in, xs2, &ldsy);
+      yin = fsw_stream<A_, D, SW>(src, dst, n, a, t, te, yin, has_in, xs2, &ldsy, &nan_at);
       has_in = true;
       serial_run += (int)(te - t);
       t = te;
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           for (int e = 0; e < W; ++e) {
             const int li = fsw_li(q, e, W);
             const S pe = e ? c[q][e - 1] : pvs[q];
-            const S r = Tr::store(Tr::step_raw(Tr::val(pe), v[q][e]));
+            const S r = Tr::store(Tr::step(Tr::val(pe), v[q][e]));
             // non-short-circuit (&): no control flow per element
             const bool ok = (Tr::bits(c[q][e]) == Tr::bits(r)) & Tr::finite(c[q][e]);
             const bool bad = (!ok) & (li > fpos) & (li < cnt) & !(q == 0 && e == 0 && lane == 0);
@@ -1078,6 +1079,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
         }
         const V last = fsw_chain<D>(xs, j, cnt, acc);
         ldsy = Tr::store(last);
+        if (D != MC_F2 && nan_at == SER_NO_NAN && __builtin_isnan(last)) nan_at = t0;  // ser_nan_fix
       }
       __syncthreads();
 #pragma unroll
@@ -1113,6 +1115,11 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
       }
     }
     ++t;
+  }
+  if constexpr (D != MC_F2) {  // numpy's NaN tail (f2 chains are exact in-chain)
+    __syncthreads();
+    if (nan_at != SER_NO_NAN)
+      ser_nan_fix<D>(src, a, dst, D | ((SW & 2) != 0 ? MC_BIG_ENDIAN : 0), n, nan_at, &nan_k0);
   }
 }
 

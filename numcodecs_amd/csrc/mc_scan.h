@@ -195,51 +195,41 @@ static inline void mc_launch_scan_sums_mw(const uint64_t *in, uint64_t *out, siz
 template <int D> struct SerAcc { using T = float; };
 template <> struct SerAcc<MC_F8> { using T = double; };
 
-// numpy's add of the running sum a and the next value b: IEEE add in D's
-// loop type with x86-64's NaN choice (mc_x86_nan: a's NaN quieted, else b's,
-// else the negative default NaN) -- the GPU's own NaN results differ (NaN +
-// NaN keeps the second operand here, inf + -inf is +NaN).  f2: numpy's half
-// loop, float32 add then npy_float_to_half (the hardware RNE conversion, with
-// denormals kept, gives the same half for every non-NaN sum; NaN sums take
-// numpy's payload-preserving routine).
+// numpy's add of the running sum a and the next value b in D's loop type.
+// f2: numpy's half loop, float32 add then npy_float_to_half (the hardware RNE
+// conversion, with denormals kept, gives the same half for every non-NaN
+// sum; NaN sums take numpy's payload-preserving routine and its operand
+// choice: the half loop keeps the SECOND operand's NaN when both are NaN --
+// measured, cumsum([NaN_a, NaN_b]) gives NaN_b for float16).  f4 / f8: the
+// plain IEEE add; where the running sum turns NaN the GPU's NaN bits differ
+// from numpy's (x86 keeps the first operand's NaN, and inf + -inf is the
+// negative default NaN there), and the chain kernels rewrite that NaN tail
+// afterwards (ser_nan_fix) instead of paying for it on the critical path.
 template <int D>
 MC_DEV typename SerAcc<D>::T ser_add(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
   if constexpr (D == MC_F2) {
-    // numpy's half loop keeps the SECOND operand's NaN when both are NaN
-    // (measured: cumsum of [NaN_a, NaN_b] gives NaN_b for float16; float32 /
-    // float64 keep the first)
     const float r = a + b;
     if (__builtin_isnan(r)) return mc_half_to_float(mc_float_to_half(mc_x86_nan(b, a, r)));
     return (float)(_Float16)r;
   } else {
-    const typename SerAcc<D>::T r = a + b;
-    return __builtin_isnan(r) ? mc_x86_nan(a, b, r) : r;
+    return a + b;
   }
-}
-// the same sum where a NaN result is only tested, never stored (the
-// speculative verification counts non-finite candidates as failures)
-template <int D>
-MC_DEV typename SerAcc<D>::T ser_add_raw(typename SerAcc<D>::T a, typename SerAcc<D>::T b) {
-  if constexpr (D == MC_F2) return ser_add<D>(a, b);
-  else return a + b;
 }
 
 // One group of the chain, in place (g[k] <- the running sum after g[k]).
 // f2: numpy adds in float32 and rounds to half; with float32's 24 >= 2*11+2
 // bits that double rounding equals one correctly rounded half add, so the
 // group runs as a chain of half adds (v_add_f16, one dependent op per
-// element; LLVM folds the float<->half round trips between them).  f4 / f8:
-// plain dependent adds.  NaN is absorbing in the chain, so a group ending in
-// NaN is recomputed with the exact routine (ser_add: numpy's payload-
-// preserving conversion, x86's NaN choice) from its first value; `src`
-// holds the group's inputs (the LDS slot the group was read from, not yet
-// overwritten) for the f4 / f8 recompute, whose in-place registers hold sums.
+// element; LLVM folds the float<->half round trips between them).  NaN is
+// absorbing in the chain, so a group ending in NaN is recomputed with the
+// exact routine (ser_add: numpy's payload-preserving conversion and NaN
+// choice) from its first value.  f4 / f8: plain dependent adds (NaN tails:
+// ser_nan_fix).
 template <int D, int G>
-MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAcc<D>::T (&g)[G],
-                                       const typename SerAcc<D>::T *src) {
+MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAcc<D>::T (&g)[G]) {
   using T = typename SerAcc<D>::T;
-  const T a0 = acc;
   if constexpr (D == MC_F2) {
+    const T a0 = acc;
     T r[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
@@ -259,18 +249,67 @@ MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAc
   } else {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      acc = acc + g[k];
+      acc = ser_add<D>(acc, g[k]);
       g[k] = acc;
-    }
-    if (__builtin_isnan(acc)) {
-      acc = a0;
-      for (int k = 0; k < G; ++k) {
-        acc = ser_add<D>(acc, src[k]);
-        g[k] = acc;
-      }
     }
   }
   return acc;
+}
+
+// ---------------------------------------------------------------------------
+// numpy's NaN tail of a float32 / float64 cumsum.  NaN is absorbing, so
+// every running sum from the first NaN one (index k0) on is NaN, and numpy's
+// loop (x86: the first operand's NaN is kept, quieted) makes them all equal
+// to the first: the NaN input at k0 quieted (a finite sum + NaN), the
+// negative default NaN (inf + -inf), or -- k0 = 0, the first element, which
+// is copied without an add -- that input quieted from k0 + 1 on.  A chain
+// kernel whose running sum ended NaN in some block calls ser_nan_fix once at
+// its end, with every thread of the workgroup, from the start of the first
+// such block: it finds k0 in dst and rewrites [k0, n) (or [1, n)) with those
+// bits, cast to the output dtype d (whose bits it writes as stored).
+// ---------------------------------------------------------------------------
+MC_DEV bool ser_is_nan_bits(uint64_t b, int d) {
+  switch (mc_dt_base(d)) {
+    case MC_F2: return (b & 0x7fffu) > 0x7c00u;
+    case MC_F4: return (b & 0x7fffffffu) > 0x7f800000u;
+    default: return (b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+  }
+}
+
+template <int L>
+MC_DEV uint64_t ser_nan_tail_bits(uint64_t e_bits, int a, int d) {
+  static_assert(L == MC_F4 || L == MC_F8, "float32 / float64 loops");
+  const McNum v = mc_num_cast(mc_num_from_bits(e_bits, a), a, L);
+  double q;
+  if (L == MC_F4) {
+    const uint32_t b = __builtin_isnan(v.f) ? (mc_f32_bits((float)v.f) | 0x00400000u) : 0xFFC00000u;
+    q = (double)mc_bits_f32(b);
+  } else {
+    q = mc_bits_f64(__builtin_isnan(v.f) ? (mc_f64_bits(v.f) | 0x0008000000000000ull) : 0xFFF8000000000000ull);
+  }
+  return mc_num_to_bits(mc_num_cast(mc_num_f(q), L, d), d);
+}
+
+constexpr size_t SER_NO_NAN = ~(size_t)0;
+
+template <int L>
+MC_DEV void ser_nan_fix(const uint8_t *src, int a, uint8_t *dst, int d, size_t n, size_t from,
+                        unsigned long long *lds) {
+  const int ds = mc_itemsize(d), as = mc_itemsize(a);
+  if (threadIdx.x == 0) *lds = ~0ull;
+  __syncthreads();
+  for (size_t b = from; b < n; b += blockDim.x) {
+    const size_t i = b + threadIdx.x;
+    if (i < n && ser_is_nan_bits(mc_to_storage(mc_load_elem_u(dst, i, ds), d), d)) atomicMin(lds, (unsigned long long)i);
+    __syncthreads();
+    const unsigned long long k = *lds;
+    __syncthreads();
+    if (k != ~0ull) break;
+  }
+  const unsigned long long k0 = *lds;
+  if (k0 >= n) return;
+  const uint64_t v = ser_nan_tail_bits<L>(mc_load_elem_u(src, (size_t)k0, as), a, d);
+  for (size_t i = (k0 == 0 ? 1 : (size_t)k0) + threadIdx.x; i < n; i += blockDim.x) mc_store_elem_u(dst, i, ds, v);
 }
 
 // G chain values as 16-B LDS accesses (p 16-B aligned)

@@ -122,6 +122,9 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
   // only loads -- the chain's LDS writes were on its critical path (13.1 ->
   // 11.0 cycles per element, tools/probe_chain.py kinds 1 and 14)
   constexpr bool DIRECT = L == D && A_ == D && VEC && !SWO && D != MC_F2;
+  __shared__ size_t nan_at;  // first block whose chain ended NaN (ser_nan_fix)
+  __shared__ unsigned long long nan_k0;
+  if (threadIdx.x == 0) nan_at = SER_NO_NAN;
   if (io) load_blk(0);
   __syncthreads();
   T acc = 0;
@@ -155,11 +158,11 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
         for (; j + 2 * SER_G <= cnt; j += 2 * SER_G) {
           ser_ld<T, SER_G>(p + j + SER_G, gb);
           __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead ahead of the adds
-          acc = ser_group<L, SER_G>(acc, ga, p + j);
+          acc = ser_group<L, SER_G>(acc, ga);
           ser_st<T, SER_G>(o + j, ga);
           ser_ld<T, SER_G>(p + j + 2 * SER_G, ga);
           __builtin_amdgcn_sched_barrier(0);
-          acc = ser_group<L, SER_G>(acc, gb, p + j + SER_G);
+          acc = ser_group<L, SER_G>(acc, gb);
           ser_st<T, SER_G>(o + j + SER_G, gb);
         }
       }
@@ -167,10 +170,15 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
         acc = ser_add<L>(acc, p[j]);
         o[j] = acc;
       }
+      if (L != MC_F2 && nan_at == SER_NO_NAN && __builtin_isnan(acc)) nan_at = b * BLK;
     }
     __syncthreads();
   }
   if (io && !DIRECT) store_blk(nb - 1);
+  if constexpr (L != MC_F2) {  // numpy's NaN tail (f2 chains are exact in-chain)
+    __syncthreads();
+    if (nan_at != SER_NO_NAN) ser_nan_fix<L>(src, a, dst, D | (SWO ? MC_BIG_ENDIAN : 0), n, nan_at, &nan_k0);
+  }
 }
 
 // (slot bytes, group) per schedule: a 32 KiB slot amortises the block

@@ -224,6 +224,64 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair(
   }
 }
 
+// es = 8, lane pairs + an LDS-staged plane side (round 5, layout V_PAIR_LDS):
+// the pair layout's plane dwords (even lanes planes 0-3, odd lanes planes 4-7
+// of 4 elements) go to a plane-major LDS image, and every lane then stores
+// 16 B of one plane -- 1 KiB contiguous per wave store instruction, against
+// two 128-B runs per instruction in the register layout.  Plane rows are
+// padded to TE/4 + 8 dwords: a write instruction's even and odd lanes (planes
+// b and b + 4, same quad index) then sit 32 banks apart, conflict-free, and
+// rows stay 16-B aligned for the ds_read_b128s.
+template <bool BITROUND, bool NT, int NV>
+__global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair_lds(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,
+    McBitRound br) {
+  constexpr int TB = NV * 16 * MC_BLOCK, TE = TB / 8;
+  constexpr int ROW = TE / 4 + 8;   // dwords per plane row in LDS
+  constexpr int PU = TE / 16;       // 16-B units per plane
+  __shared__ __attribute__((aligned(16))) uint32_t lds[8 * ROW];
+  const int tid = threadIdx.x;
+  const bool odd = tid & 1;
+  MC_FOR_TILES(tile, ntiles, m) {
+    const size_t c = tile / m.tiles_per_chunk;
+    const size_t t = tile - c * m.tiles_per_chunk;
+    const uint8_t *s = src + c * m.src_stride + t * (size_t)TB;
+    uint8_t *d = dst + c * m.dst_stride + t * (size_t)TE;
+    mc_u32x4 v[NV];
+#pragma unroll
+    for (int r = 0; r < NV; ++r) v[r] = mc_ld16<NT>(s + ((size_t)r * MC_BLOCK + tid) * 16);
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      mc_u32x4 x = v[r];
+      if constexpr (BITROUND) {
+        uint64_t e0 = mc_bitround64(((uint64_t)x.y << 32) | x.x, br);
+        uint64_t e1 = mc_bitround64(((uint64_t)x.w << 32) | x.z, br);
+        x = mc_u32x4{(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)e1, (uint32_t)(e1 >> 32)};
+      }
+      const uint32_t a = mc_pair_swap(odd ? x.x : x.y);
+      const uint32_t b = mc_pair_swap(odd ? x.z : x.w);
+      uint32_t p0, p1, p2, p3;
+      if (odd) mc_tr4(a, b, x.y, x.w, p0, p1, p2, p3);   // high dwords of e0..e3
+      else mc_tr4(x.x, x.z, a, b, p0, p1, p2, p3);       // low dwords of e0..e3
+      const int qi = r * (MC_BLOCK / 2) + (tid >> 1);    // quad index in the tile
+      uint32_t *row = lds + (odd ? 4 * ROW : 0) + qi;
+      row[0] = p0;
+      row[ROW] = p1;
+      row[2 * ROW] = p2;
+      row[3 * ROW] = p3;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+      const int u = r * MC_BLOCK + tid;
+      const int pb = u / PU, j = u - pb * PU;
+      const mc_u32x4 o = *reinterpret_cast<const mc_u32x4 *>(lds + pb * ROW + 4 * j);
+      mc_st16<NT>(d + (size_t)pb * m.count + (size_t)j * 16, o);
+    }
+    __syncthreads();
+  }
+}
+
 template <bool NT, int NV>
 __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_dec_pair(
     const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles) {
@@ -627,7 +685,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle_dec_generic(
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4, V_PAIR = 5, V_WIDE = 6 };
+enum Variant { V_DEFAULT = 0, V_REG = 1, V_PLANE_LDS = 2, V_BOTH_LDS = 3, V_GENERIC = 4, V_PAIR = 5, V_WIDE = 6,
+               V_PAIR_LDS = 7 };
 // variant | V_NO_NT selects default-policy (temporal) global accesses
 static constexpr int V_NO_NT = 8;
 // variant | V_BIG selects 2x larger tiles, | V_BIG4 4x (register layout only)
@@ -711,6 +770,12 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
       else k_shuffle8_enc_quad<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       return;
     }
+    if ((layout & 7) == V_PAIR_LDS) {
+      if (layout & V_BIG4) k_shuffle8_enc_pair_lds<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else if (layout & V_BIG) k_shuffle8_enc_pair_lds<BR, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      else k_shuffle8_enc_pair_lds<BR, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
+      return;
+    }
     if ((layout & 7) == V_PAIR) {
       if (layout & V_BIG8) k_shuffle8_enc_pair<BR, NT, 32><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
       else if (layout & V_BIG4) k_shuffle8_enc_pair<BR, NT, 16><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br);
@@ -744,8 +809,9 @@ static int launch_enc_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
                             size_t ntiles, unsigned grid, const McBitRound &br,
                             hipStream_t st) {
   const int layout = variant & (7 | V_TILE_MASK | V_PIPE);
-  if ((layout & 7) < V_REG || (layout & 7) > V_WIDE || (layout & 7) == V_GENERIC) return MC_EINVAL;
+  if ((layout & 7) < V_REG || (layout & 7) == V_GENERIC) return MC_EINVAL;
   if ((layout & 7) == V_PAIR && ES != 8 && ES != 4) return MC_EINVAL;
+  if ((layout & 7) == V_PAIR_LDS && (ES != 8 || (layout & (V_PIPE | V_BIG8)))) return MC_EINVAL;
   if ((layout & 7) == V_WIDE && ((ES != 4 && ES != 8) || (layout & (V_PIPE | V_BIG8)))) return MC_EINVAL;
   if ((layout & V_BIG8) && (layout & V_PIPE)) return MC_EINVAL;
   if (variant & V_NO_NT) launch_enc_nt<ES, BR, false>(layout, s, d, m, ntiles, grid, br, st);
@@ -816,9 +882,10 @@ static int launch_dec_tiles(int variant, const uint8_t *s, uint8_t *d, const Chu
 
 static size_t tile_elems(size_t es, int variant) {
   const size_t mul = (variant & V_BIG8) ? 8 : (variant & V_BIG4) ? 4 : (variant & V_BIG) ? 2 : 1;
-  if (((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) && es == 4)  // Geom<4, QMUL> tiles
+  const bool pairish = (variant & 7) == V_PAIR || (variant & 7) == V_WIDE || (variant & 7) == V_PAIR_LDS;
+  if (pairish && es == 4)  // Geom<4, QMUL> tiles
     return 4096 * mul;
-  if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE)  // 256 lanes x NV 16-B units of 8-B elements
+  if (pairish)  // 256 lanes x NV 16-B units of 8-B elements
     return 2048 * mul;
   const size_t te = es >= 16 ? 2048 : 4096;
   if ((variant & 7) != V_REG) return te;
@@ -869,11 +936,12 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   const McBitRound &brr = br ? *br : nobr;
   if ((variant & 7) != V_GENERIC) {
     if ((variant & 7) == V_PAIR && es != 8 && es != 4) variant = V_REG | (variant & V_NO_NT);
+    if ((variant & 7) == V_PAIR_LDS && (es != 8 || !enc)) variant = V_REG | (variant & V_NO_NT);
     if ((variant & 7) == V_WIDE && !(es == 8 || (es == 4 && enc))) variant = V_REG | (variant & V_NO_NT);
-    if ((variant & 7) != V_REG && (variant & 7) != V_PAIR && (variant & 7) != V_WIDE)
+    if ((variant & 7) != V_REG && (variant & 7) != V_PAIR && (variant & 7) != V_WIDE && (variant & 7) != V_PAIR_LDS)
       variant &= ~(V_TILE_MASK | V_PIPE);
-    if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE) variant &= ~V_PIPE;
-    if ((variant & 7) == V_WIDE || es == 16) variant &= ~V_BIG8;
+    if ((variant & 7) == V_PAIR || (variant & 7) == V_WIDE || (variant & 7) == V_PAIR_LDS) variant &= ~V_PIPE;
+    if ((variant & 7) == V_WIDE || (variant & 7) == V_PAIR_LDS || es == 16) variant &= ~V_BIG8;
     if (variant & V_PIPE) variant &= ~(V_GROUP_MASK | V_BIG8);
     if (variant & V_BIG8) variant &= ~(V_BIG | V_BIG4);
     if (variant & V_BIG4) variant &= ~V_BIG;

@@ -59,9 +59,30 @@ def test_lab_chain_kinds_write_numpy_cumsum(device):
     cyc = torch.zeros(2, dtype=torch.int64, device=device)
     gin = torch.randn(n, device=device)
     want = np.cumsum(gin.cpu().numpy())
-    for kind in (13, 15, 16, 17, 18, 20, 23):  # (14, 24, 25 chain over their LDS init, not gin)
+    # (14, 24, 25 chain over their LDS init, not gin; 21 / 22 store each group
+    # one group late -- round 4 left the last group unstored, fixed in round 5)
+    for kind in (13, 15, 16, 17, 18, 20, 21, 22, 23):
         gout = torch.zeros(n, device=device)
         assert lab.mc_lab_chain_g(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, 1, kind, gin.data_ptr(),
                                   gout.data_ptr(), st) == 0
         torch.cuda.synchronize()
         assert np.array_equal(gout.cpu().numpy().view(np.uint32), want.view(np.uint32)), kind
+
+
+def test_lab_chain64_kinds_write_numpy_cumsum(device):
+    """The f64 chain schedules that store (kinds 42-44) write numpy's float64
+    cumsum of their input, bit for bit."""
+    lab = lab_lib()
+    st = torch.cuda.current_stream().cuda_stream
+    n = 4096
+    init = torch.arange(64, device=device, dtype=torch.float64) * 1e-3
+    out = torch.empty(4, device=device, dtype=torch.float64)
+    cyc = torch.zeros(2, dtype=torch.int64, device=device)
+    gin = torch.randn(n, device=device, dtype=torch.float64)
+    want = np.cumsum(gin.cpu().numpy())
+    for kind in (42, 43, 44):
+        gout = torch.zeros(n, device=device, dtype=torch.float64)
+        assert lab.mc_lab_chain64(init.data_ptr(), out.data_ptr(), cyc.data_ptr(), n, 1, kind, gin.data_ptr(),
+                                  gout.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(gout.cpu().numpy().view(np.uint64), want.view(np.uint64)), kind

@@ -331,6 +331,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_lab_chain_sgpr(const float *__re
           st(jj, ra);
           __builtin_amdgcn_sched_barrier(0);
         }
+        // the last group's results are still pending (round 4 left them out:
+        // the "one group late" store of the first group wrote zeros there)
+        st(n - SG, rb);
       }
     } else {
       // 4 result sets: group t writes S[t % 4], the stores of S[(t-1) % 4]
@@ -364,6 +367,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_lab_chain_sgpr(const float *__re
             for (int k = 0; k < SG; ++k) asm volatile("" ::"v"(S[(u + 2) & 3][k]));
           }
         }
+        st(n - SG, S[3]);  // the last group (stored one group late, after the loop)
       }
     }
   } else {
@@ -442,7 +446,132 @@ __global__ __launch_bounds__(64 * WAVES) void k_lab_chain_sgpr(const float *__re
   }
 }
 
+// ---------------------------------------------------------------------------
+// f64 chains (round 5): the dependent v_add_f64 floor and the SGPR-fed /
+// LDS-fed schedules of the product's f8 walker, one wave
+//   kind 40  register-only chain
+//   kind 41  SGPR-fed (s_load of the inputs), no result stores
+//   kind 42  SGPR-fed, every lane stores the (uniform) results, 16-B stores
+//   kind 43  LDS-fed, lane 0 stores to global (the product's f8 fsw_chain)
+//   kind 44  SGPR-fed, lane 0 stores to global
+// ---------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) double *cdp;
+
+template <int KIND>
+__global__ __launch_bounds__(64) void k_lab_chain64(const double *__restrict__ init, double *__restrict__ out,
+                                                   long long *__restrict__ cyc, int n, int reps,
+                                                   const double *__restrict__ gin, double *__restrict__ gout) {
+  constexpr int SG = 16;  // values per group
+  __shared__ __attribute__((aligned(16))) double p[4096 + 4 * SG];
+  for (int i = threadIdx.x; i < n + 4 * SG; i += 64) p[i] = i < n ? gin[i] : init[i % 64];
+  __syncthreads();
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  if constexpr (KIND == 40) {
+    if (lane == 0) {
+      double v[16];
+      for (int k = 0; k < 16; ++k) v[k] = p[k];
+      for (int r = 0; r < reps; ++r)
+        for (int j = 0; j < n; j += 16) {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) acc = acc + v[k];
+          v[j & 15] = acc;
+        }
+    }
+  } else if constexpr (KIND == 43) {
+    if (lane == 0) {
+      for (int r = 0; r < reps; ++r) {
+        double ga[SG], gb[SG];
+        ser_ld<double, SG>(p, ga);
+        for (int j = 0; j + 2 * SG <= n; j += 2 * SG) {
+          ser_ld<double, SG>(p + j + SG, gb);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < SG; ++k) {
+            acc = acc + ga[k];
+            ga[k] = acc;
+          }
+          ser_st<double, SG>(gout + j, ga);
+          ser_ld<double, SG>(p + j + 2 * SG, ga);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int k = 0; k < SG; ++k) {
+            acc = acc + gb[k];
+            gb[k] = acc;
+          }
+          ser_st<double, SG>(gout + j + SG, gb);
+        }
+      }
+    }
+  } else {
+    cdp src = (cdp)gin;
+    auto sld = [&](int at, double (&g)[SG]) {
+#pragma unroll
+      for (int k = 0; k < SG; ++k) g[k] = src[at + k];
+    };
+    auto group = [&](int j, const double (&g)[SG]) {
+      double res[SG];
+#pragma unroll
+      for (int k = 0; k < SG; ++k) {
+        acc = acc + g[k];
+        res[k] = acc;
+      }
+      if constexpr (KIND == 42) {
+#pragma unroll
+        for (int k = 0; k < SG / 2; ++k) reinterpret_cast<d2v *>(gout + j)[k] = d2v{res[2 * k], res[2 * k + 1]};
+      } else if constexpr (KIND == 44) {
+        if (lane == 0) {
+#pragma unroll
+          for (int k = 0; k < SG / 2; ++k) reinterpret_cast<d2v *>(gout + j)[k] = d2v{res[2 * k], res[2 * k + 1]};
+        }
+      } else {
+        (void)res;
+      }
+    };
+    for (int r = 0; r < reps; ++r) {
+      double ga[SG], gb[SG];
+      sld(0, ga);
+      for (int j = 0; j < n; j += 2 * SG) {
+        const int jj = __builtin_amdgcn_readfirstlane(j);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        sld(jj + SG, gb);
+        __builtin_amdgcn_sched_barrier(0);
+        group(jj, ga);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        sld((jj + 2 * SG) & (n - 1), ga);
+        __builtin_amdgcn_sched_barrier(0);
+        group(jj + SG, gb);
+      }
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    out[0] = acc + p[7];
+    cyc[0] = t1 - t0;
+  }
+}
+
 }  // namespace
+
+extern "C" int mc_lab_chain64(const double *init, double *out, long long *cyc, int n, int reps, int kind,
+                              const double *gin, double *gout, mc_stream_t stream) {
+  if (n <= 0 || n > 4096 || (n & (n - 1)) || n < 64 || reps <= 0) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  switch (kind) {
+    case 40: k_lab_chain64<40><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 41: k_lab_chain64<41><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 42: k_lab_chain64<42><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 43: k_lab_chain64<43><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    case 44: k_lab_chain64<44><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
+    default: return MC_EINVAL;
+  }
+  return mc_last_launch();
+}
 
 extern "C" int mc_lab_chain(const float *init, float *out, long long *cyc, int n, int reps, int kind,
                             mc_stream_t stream) {

@@ -54,6 +54,41 @@ def main():
         if not np.array_equal(gout.cpu().numpy().view(np.uint32), want.view(np.uint32)):
             bad.append(kind)
     print("chain correctness failures:", bad, flush=True)
+    # f64 kinds (round 5): correctness of the stored kinds, then timing
+    n64 = 4096
+    gin64 = torch.randn(n64, device=dev, dtype=torch.float64)
+    gout64 = torch.zeros(n64, device=dev, dtype=torch.float64)
+    init64 = torch.arange(64, device=dev, dtype=torch.float64) * 1e-3
+    out64 = torch.empty(4, device=dev, dtype=torch.float64)
+
+    def run64(kind, r=reps):
+        return lab.mc_lab_chain64(init64.data_ptr(), out64.data_ptr(), cyc.data_ptr(), n64, r, kind,
+                                  gin64.data_ptr(), gout64.data_ptr(), st)
+
+    want64 = np.cumsum(gin64.cpu().numpy())
+    bad64 = []
+    for kind in (42, 43, 44):
+        gout64.zero_()
+        assert run64(kind, 1) == 0
+        torch.cuda.synchronize()
+        if not np.array_equal(gout64.cpu().numpy().view(np.uint64), want64.view(np.uint64)):
+            bad64.append(kind)
+    print("f64 chain correctness failures:", bad64, flush=True)
+    for rnd in range(3):
+        for kind, name in ((40, "f64 register-only"), (41, "f64 SGPR-fed, no stores"),
+                           (42, "f64 SGPR-fed, all-lane stores"), (43, "f64 LDS-fed, lane-0 global stores"),
+                           (44, "f64 SGPR-fed, lane-0 global stores")):
+            assert run64(kind) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert run64(kind) == 0
+            e1.record()
+            e1.synchronize()
+            t = e0.elapsed_time(e1) * 1e-3
+            el = n64 * reps
+            print(json.dumps({"round": rnd, "kind": kind, "name": name, "Melem_per_s": round(el / t / 1e6, 1),
+                              "ticks_per_elem": round(int(cyc[0].item()) / el, 3), "us": round(t * 1e6, 1)}),
+                  flush=True)
     rows = []
     for rnd in range(3):
         for kind in NAMES:

@@ -19,11 +19,13 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from lab.lablib import lab as _lab  # noqa: E402
 
 V_REG, V_WIDE, V_PAIR, V_NO_NT, V_BIG, V_BIG4, V_PIPE, V_BIG8 = 1, 6, 5, 8, 16, 128, 256, 512
+V_PAIR_LDS = 7  # round 5: lane pairs + LDS-staged 16-B plane stores (es = 8)
 LAYOUTS = {
     4: [V_REG | V_BIG8, V_REG | V_BIG4, V_REG | V_BIG, V_REG, V_REG | V_PIPE | V_BIG4, V_REG | V_PIPE | V_BIG,
         V_PAIR | V_BIG8, V_PAIR | V_BIG4, V_PAIR | V_BIG, V_PAIR, V_WIDE | V_BIG, V_WIDE | V_BIG4,
         V_REG | V_BIG8 | V_NO_NT, V_PAIR | V_BIG4 | V_NO_NT],
-    8: [V_PAIR, V_PAIR | V_BIG, V_PAIR | V_BIG4, V_PAIR | V_BIG8, V_REG, V_REG | V_BIG, V_REG | V_BIG4, V_REG | V_BIG8,
+    8: [V_PAIR, V_PAIR_LDS, V_PAIR_LDS | V_BIG, V_PAIR_LDS | V_BIG4, V_PAIR_LDS | V_NO_NT,
+        V_PAIR | V_BIG, V_PAIR | V_BIG4, V_PAIR | V_BIG8, V_REG, V_REG | V_BIG, V_REG | V_BIG4, V_REG | V_BIG8,
         V_REG | V_PIPE, V_REG | V_PIPE | V_BIG, V_WIDE, V_WIDE | V_BIG, V_WIDE | V_BIG4, V_PAIR | V_NO_NT,
         V_REG | V_NO_NT, V_REG | V_BIG4 | V_NO_NT],
 }
