@@ -194,10 +194,10 @@ MC_DEV void tr32x32(uint32_t (&a)[32]) {
 }
 
 // the thread's 8*ES plane dwords from its 32 elements' 8*ES dwords (ES = 4:
-// one transpose; ES = 8: the low and the high dword of every element), and
-// back (the transpose is an involution)
+// one transpose; ES = 8: the low and the high dword of every element),
+// stored as each half is ready (no second 8*ES-dword array: ES = 8 spilled)
 template <int ES>
-MC_DEV void bf_planes_tr(const uint32_t (&w)[8 * ES], uint32_t (&pl)[8 * ES]) {
+MC_DEV void bf_planes_store(const uint32_t (&w)[8 * ES], uint8_t *pd, size_t pstride) {
   static_assert(ES == 4 || ES == 8, "32x32 transposes for 4- and 8-byte elements");
 #pragma unroll
   for (int h = 0; h < ES / 4; ++h) {
@@ -206,16 +206,19 @@ MC_DEV void bf_planes_tr(const uint32_t (&w)[8 * ES], uint32_t (&pl)[8 * ES]) {
     for (int i = 0; i < 32; ++i) a[i] = w[(ES / 4) * i + h];
     tr32x32(a);
 #pragma unroll
-    for (int p = 0; p < 32; ++p) pl[32 * h + p] = a[p];
+    for (int p = 0; p < 32; ++p)
+      __builtin_nontemporal_store(a[p], reinterpret_cast<uint32_t *>(pd + (size_t)(32 * h + p) * pstride));
   }
 }
+// and back (the transpose is an involution): plane dwords loaded half by half
 template <int ES>
-MC_DEV void bf_elems_tr(const uint32_t (&pl)[8 * ES], uint32_t (&w)[8 * ES]) {
+MC_DEV void bf_planes_load(const uint8_t *ps, size_t pstride, uint32_t (&w)[8 * ES]) {
 #pragma unroll
   for (int h = 0; h < ES / 4; ++h) {
     uint32_t a[32];
 #pragma unroll
-    for (int p = 0; p < 32; ++p) a[p] = pl[32 * h + p];
+    for (int p = 0; p < 32; ++p)
+      a[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)(32 * h + p) * pstride));
     tr32x32(a);
 #pragma unroll
     for (int i = 0; i < 32; ++i) w[(ES / 4) * i + h] = a[i];
@@ -251,11 +254,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__r
     }
     uint8_t *pd = d + gw + BF_GPT * (size_t)t;
     if constexpr (ES == 4 || ES == 8) {
-      uint32_t pl[8 * ES];
-      bf_planes_tr<ES>(w, pl);
-#pragma unroll
-      for (int p = 0; p < 8 * ES; ++p)
-        __builtin_nontemporal_store(pl[p], reinterpret_cast<uint32_t *>(pd + (size_t)p * pstride));
+      bf_planes_store<ES>(w, pd, pstride);
       return;
     }
 #pragma unroll
@@ -280,13 +279,14 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__r
     uint32_t w[8 * ES];
     if (t < nthr) {
       const uint8_t *ps = s + gw + BF_GPT * (size_t)t;
+      if constexpr (ES == 4 || ES == 8) {
+        bf_planes_load<ES>(ps, pstride, w);
+      } else {
       uint32_t pl[8 * ES];
 #pragma unroll
       for (int p = 0; p < 8 * ES; ++p)
         pl[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)p * pstride));
-      if constexpr (ES == 4 || ES == 8) {
-        bf_elems_tr<ES>(pl, w);
-      } else {
+
 #pragma unroll
       for (int i = 0; i < 8 * ES; ++i) w[i] = 0;
 #pragma unroll

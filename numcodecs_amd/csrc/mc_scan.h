@@ -256,6 +256,120 @@ MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAc
   return acc;
 }
 
+// a pointer the compiler may keep in SGPRs (the value is wave-uniform)
+template <typename P>
+MC_DEV P *mc_uniform_ptr(P *p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return reinterpret_cast<P *>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
+// ---------------------------------------------------------------------------
+// The chain fed through VGPRs by uniform-address vector loads (round 5): every
+// lane of the calling wave loads the same 16 B per instruction, runs the same
+// dependent adds on VGPR operands and stores the same results as 16-B
+// vectors -- no lane-0 branch and no LDS staging of the inputs.  Vector loads
+// return in order, so D groups of SG values stay in flight (the compiler's
+// vmcnt(N) waits only for the group about to be added), which hides HBM's
+// latency without a prefetching wave.  In the product's noise-like float32
+// Delta decode (k_fspec_walk, 256 MiB) it runs at 294 ms against 325-360 ms
+// for the LDS-fed lane-0 chain and 325 ms for a scalar-load (SGPR operand)
+// chain with an L2-prefetching wave (tools/lab/lab_chain.hip,
+// tools/probe_stream.py).  The scalar chain is the fastest on cache-resident
+// input (lab kinds 23 / 42), but scalar loads return out of order (any wait
+// is lgkmcnt(0)), so it keeps only one group in flight and its per-group L2
+// latency bounds it when streaming.  For float64 the LDS-fed chain stays
+// faster in the walker (228 vs 259 ms on one box): the all-lane 16-B loads
+// and stores, one per two elements, cost more issue time than its lane-0
+// LDS reads.  `in` and `out` must have the same address modulo 16 (the
+// callers check).
+// ---------------------------------------------------------------------------
+template <typename T, int SG, int D>
+MC_DEV T ser_chain_vbc(const T *in, T *out, size_t cnt, T acc) {
+  constexpr int W = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(W)));
+  typedef __attribute__((address_space(1))) T *gp;
+  typedef __attribute__((address_space(1))) vec *gvp;
+  typedef const __attribute__((address_space(1))) vec *cgvp;
+  typedef const __attribute__((address_space(1))) T *cgp;
+  int z;  // a zero the compiler cannot prove uniform: the loads stay vector loads
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  const cgp src = (cgp)(in + z);
+  const gp dstp = (gp)mc_uniform_ptr(out);
+  // a short run [j, j + m) (m <= SG), its loads issued together
+  auto run = [&](size_t j, int m) {
+    T v[SG];
+#pragma unroll
+    for (int k = 0; k < SG; ++k) v[k] = k < m ? src[j + k] : (T)0;
+#pragma unroll
+    for (int k = 0; k < SG; ++k)
+      if (k < m) {
+        acc = acc + v[k];
+        dstp[j + k] = acc;
+      }
+  };
+  size_t j = 0;
+  {
+    const int h = (int)(((16 - ((uintptr_t)out & 15)) & 15) / sizeof(T));
+    const int m = (size_t)h < cnt ? h : (int)cnt;
+    if (m > 0) run(0, m);
+    j = m;
+  }
+  auto ld = [&](size_t at, T(&g)[SG]) {
+    const cgvp q = (cgvp)(src + at);
+#pragma unroll
+    for (int k = 0; k < SG / W; ++k) {
+      const vec x = q[k];
+#pragma unroll
+      for (int e = 0; e < W; ++e) g[W * k + e] = x[e];
+    }
+  };
+  auto grp = [&](size_t at, const T(&g)[SG]) {
+    T res[SG];
+#pragma unroll
+    for (int k = 0; k < SG; ++k) {
+      acc = acc + g[k];
+      res[k] = acc;
+    }
+    const gvp o = (gvp)(dstp + at);
+#pragma unroll
+    for (int k = 0; k < SG / W; ++k) {
+      vec x;
+#pragma unroll
+      for (int e = 0; e < W; ++e) x[e] = res[W * k + e];
+      o[k] = x;
+    }
+  };
+  if (j + (size_t)D * SG <= cnt) {
+    T buf[D][SG];
+#pragma unroll
+    for (int u = 0; u < D; ++u) ld(j + (size_t)u * SG, buf[u]);
+    for (; j + 2 * (size_t)D * SG <= cnt; j += (size_t)D * SG) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        grp(j + (size_t)u * SG, buf[u]);
+        ld(j + (size_t)(u + D) * SG, buf[u]);
+      }
+    }
+    // the last loaded round, the remaining whole groups loaded behind it
+    const size_t j2 = j + (size_t)D * SG;
+    const int ng = (int)((cnt - j2) / SG);  // < D
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      grp(j + (size_t)u * SG, buf[u]);
+      if (u < ng) ld(j2 + (size_t)u * SG, buf[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (u < ng) grp(j2 + (size_t)u * SG, buf[u]);
+    j = j2 + (size_t)ng * SG;
+  }
+  for (; j < cnt; j += SG) run(j, cnt - j < (size_t)SG ? (int)(cnt - j) : SG);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
 // numpy's NaN tail of a float32 / float64 cumsum.  NaN is absorbing, so
 // every running sum from the first NaN one (index k0) on is NaN, and numpy's

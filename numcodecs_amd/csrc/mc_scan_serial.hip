@@ -117,14 +117,34 @@ __global__ __launch_bounds__(128) void k_scan_serial(const uint8_t *__restrict__
     }
   };
 
-  // same-type little-endian f4 / f8 with vector access: the chain lane
-  // stores its results straight to dst (16-B global stores), the I/O wave
-  // only loads -- the chain's LDS writes were on its critical path (13.1 ->
-  // 11.0 cycles per element, tools/probe_chain.py kinds 1 and 14)
+  // same-type little-endian f4 / f8 with vector access: ser_chain_vbc for f4
+  // when src and dst are equally 16-B aligned (as in k_fspec_walk's
+  // fsw_stream); otherwise the LDS-fed chain below,
+  // whose chain lane stores its results straight to dst (16-B global
+  // stores) while the I/O wave only loads -- the chain's LDS writes were on
+  // its critical path (13.1 -> 11.0 cycles per element, tools/probe_chain.py
+  // kinds 1 and 14)
   constexpr bool DIRECT = L == D && A_ == D && VEC && !SWO && D != MC_F2;
   __shared__ size_t nan_at;  // first block whose chain ended NaN (ser_nan_fix)
   __shared__ unsigned long long nan_k0;
   if (threadIdx.x == 0) nan_at = SER_NO_NAN;
+  if constexpr (DIRECT) {
+    if (sizeof(T) == 4 && ((uintptr_t)src & 15) == ((uintptr_t)dst & 15)) {
+      // one chain over the whole chunk by wave 0, straight from src to dst
+      // (ser_chain_vbc); the I/O wave has nothing to stage
+      if (!io) {
+        const T *in = reinterpret_cast<const T *>(src);
+        T *out = reinterpret_cast<T *>(dst);
+        T acc = has_carry ? ser_add<L>(carry, in[0]) : in[0];
+        out[0] = acc;
+        acc = ser_chain_vbc<T, sizeof(T) == 8 ? 16 : 32, 6>(in + 1, out + 1, n - 1, acc);
+        if (threadIdx.x == 0 && __builtin_isnan(acc)) nan_at = 0;
+      }
+      __syncthreads();
+      if (nan_at != SER_NO_NAN) ser_nan_fix<L>(src, a, dst, D, n, 0, &nan_k0);
+      return;
+    }
+  }
   if (io) load_blk(0);
   __syncthreads();
   T acc = 0;

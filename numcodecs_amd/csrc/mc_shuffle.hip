@@ -232,6 +232,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair(
 // padded to TE/4 + 8 dwords: a write instruction's even and odd lanes (planes
 // b and b + 4, same quad index) then sit 32 banks apart, conflict-free, and
 // rows stay 16-B aligned for the ds_read_b128s.
+// Measured (tools/probe_enc_variants.py, 256 MiB): 99.7 us against 91.5 us
+// for V_PAIR (BIG 108, BIG4 105, NO_NT 99.6): the LDS round trip costs more
+// than the wider stores save.  Kept as a selectable variant, never the default.
 template <bool BITROUND, bool NT, int NV>
 __global__ __launch_bounds__(MC_BLOCK) void k_shuffle8_enc_pair_lds(
     const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, ChunkMap m, size_t ntiles,

@@ -556,6 +556,170 @@ __global__ __launch_bounds__(64) void k_lab_chain64(const double *__restrict__ i
   }
 }
 
+// ---------------------------------------------------------------------------
+// LAB: the chain fed from SGPRs (round 5, lab kinds 23 / 42,
+// profiles/r05/probe_chain_r5.jsonl): every lane of the calling wave runs the
+// same dependent adds, the operands coming from scalar loads straight out of
+// global memory (s_load_dwordxN: no VGPR or LDS staging of the inputs, the
+// adds read SGPRs), and every lane stores the (uniform) results as 16-B
+// vectors to the same addresses -- no lane-0 branch for the compiler to sink
+// the adds past.  Measured per element: f32 9.4 ticks against 11.0 for the
+// LDS-fed lane-0 chain, f64 14.9 against 18.7.  Two scalar groups of SG
+// values alternate, the next group's loads issued after the current group's
+// have landed (scalar loads return out of order: any wait is lgkmcnt(0)).
+// `in` / `out`: element pointers (uniform), `out` 16-B aligned; cnt elements.
+// Only for f4 / f8 with astype == dtype, little-endian.
+// ---------------------------------------------------------------------------
+// `prog` (LDS, may be null): the chain publishes how many of the cnt
+// elements it has consumed, for ser_prefetch in another wave.
+template <typename T, int SG = sizeof(T) == 8 ? 16 : 32>  // SG: values per scalar group
+MC_DEV T ser_chain_sgpr(const T *in, T *out, size_t cnt, T acc, volatile size_t *prog = nullptr) {
+  constexpr int W = 16 / (int)sizeof(T);
+  typedef const __attribute__((address_space(4))) T *cp;
+  typedef T vec __attribute__((ext_vector_type(W)));
+  // stores through a global (not flat) pointer: flat stores count in
+  // lgkmcnt too, so the lgkmcnt(0) waits for the scalar loads would also
+  // wait for every store to land
+  typedef __attribute__((address_space(1))) T *gp;
+  typedef __attribute__((address_space(1))) vec *gvp;
+  in = mc_uniform_ptr(in);
+  const gp dstp = (gp)mc_uniform_ptr(out);
+  const cp src = (cp)in;
+  size_t j = 0;
+  // head: up to the first 16-B aligned output element
+  for (; j < cnt && (((uintptr_t)(out + j)) & 15); ++j) {
+    acc = acc + src[j];
+    dstp[j] = acc;
+  }
+  auto sld = [&](size_t at, T(&g)[SG]) {
+    const cp q = mc_uniform_ptr(src + at);
+#pragma unroll
+    for (int k = 0; k < SG; ++k) g[k] = q[k];
+  };
+  auto group = [&](size_t at, const T(&g)[SG]) {
+    T res[SG];
+#pragma unroll
+    for (int k = 0; k < SG; ++k) {
+      acc = acc + g[k];
+      res[k] = acc;
+    }
+    const gvp o = (gvp)(dstp + at);
+#pragma unroll
+    for (int k = 0; k < SG / W; ++k) {
+      vec v;
+#pragma unroll
+      for (int e = 0; e < W; ++e) v[e] = res[W * k + e];
+      o[k] = v;
+    }
+  };
+  if (j + 2 * SG <= cnt) {
+    T ga[SG], gb[SG];
+    sld(j, ga);
+    for (; j + 2 * SG <= cnt; j += 2 * SG) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): group ga has landed
+      __builtin_amdgcn_sched_barrier(0);
+      sld(j + SG, gb);
+      if (prog) *(volatile __attribute__((address_space(3))) size_t *)prog = j;
+      __builtin_amdgcn_sched_barrier(0);
+      group(j, ga);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 3 * SG <= cnt) sld(j + 2 * SG, ga);  // never past the input
+      __builtin_amdgcn_sched_barrier(0);
+      group(j + SG, gb);
+    }
+  }
+  for (; j < cnt; ++j) {
+    acc = acc + src[j];
+    dstp[j] = acc;
+  }
+  return acc;
+}
+
+// The scalar loads above see HBM's miss latency (~900 cycles) once per
+// group, longer than a group's adds (32 x ~9 cycles): a 256 MiB f4 chain ran
+// at 720 ms, against 360 ms for the LDS-fed one.  Scalar returns come back
+// out of order, so the chain cannot keep more than one group in flight; one
+// other wave of the workgroup instead keeps its input ahead of it in the
+// caches: vector loads (one dword per 128-B line) SER_PF_L2 bytes past the
+// chain's published position pull the lines into L2, and scalar loads (one
+// dword per 64-B line) SER_PF_K bytes past it pull them into the CU's scalar
+// cache, where the chain's own scalar loads then hit.  The wave sleeps while
+// it is that far ahead, never blocks the chain, and ends once the whole input
+// is requested (the chain's last published position is within 2 groups of
+// the end, so both windows reach it) or the chain signals its end (~0).
+// ---------------------------------------------------------------------------
+constexpr size_t SER_PF_L2 = 32768;
+constexpr size_t SER_PF_K = 0;  // the scalar-cache window: off (see below)
+
+MC_DEV void ser_prefetch(const void *in, size_t bytes, size_t es, volatile size_t *prog,
+                         size_t l2_ahead = SER_PF_L2, size_t k_ahead = SER_PF_K) {
+  typedef const __attribute__((address_space(4))) uint32_t *cp;
+  const int lane = threadIdx.x & 63;
+  const uint8_t *base = mc_uniform_ptr(reinterpret_cast<const uint8_t *>((uintptr_t)in & ~(uintptr_t)127));
+  const size_t span = bytes + ((uintptr_t)in & 127);
+  size_t pf2 = 0, pfk = 0;
+  uint32_t seen = 0;  // keeps the loads (a value no one reads)
+  if (k_ahead == 0) pfk = span;
+  while (pf2 < span || pfk < span) {
+    const size_t at = *prog;
+    if (at == ~(size_t)0) break;  // the chain has finished (k_lab_stream)
+    const size_t pos = at * es;
+    const size_t t2 = pos + l2_ahead < span ? pos + l2_ahead : span;
+    const size_t tk = pos + k_ahead < span ? pos + k_ahead : span;
+    bool idle = true;
+    if (pf2 < t2) {
+      const size_t o = pf2 + (size_t)lane * 128;
+      if (o < span) seen ^= *reinterpret_cast<const uint32_t *>(base + o);
+      pf2 += 64 * 128;
+      idle = false;
+    }
+    if (pfk < tk) {
+      const cp q = (cp)(base + pfk);
+      uint32_t k = 0;
+#pragma unroll
+      for (int l = 0; l < 16; ++l)
+        if (pfk + 64 * l < span) k ^= q[16 * l];
+      seen ^= k;
+      pfk += 16 * 64;
+      idle = false;
+    }
+    if (idle) __builtin_amdgcn_s_sleep(2);
+  }
+  __shared__ uint32_t sink;
+  if (seen == 0x9E3779B9u) sink = seen;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming chains (round 5): the lab's ser_chain_sgpr above (kinds 0 f32,
+// 1 f64) or ser_chain_vbc (kinds 2 f32, 3 f64; `ka` = its depth D) over a
+// large buffer (HBM, not cache-resident like kinds 11-25), wave 1 running
+// ser_prefetch with the given windows (pf = 0: no prefetch wave).  Finds the
+// group size and prefetch distances that hide the loads' latency.
+// ---------------------------------------------------------------------------
+template <typename T, int SG, int VD = 0>
+__global__ __launch_bounds__(128) void k_lab_stream(const T *__restrict__ in, T *__restrict__ out, size_t n,
+                                                    size_t l2a, size_t ka, int pf, long long *__restrict__ cyc) {
+  __shared__ size_t prog;
+  if (threadIdx.x == 0) prog = 0;
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x < 64) {
+    T acc = in[0];
+    if (threadIdx.x == 0) out[0] = acc;
+    if constexpr (VD > 0) acc = ser_chain_vbc<T, SG, VD>(in + 1, out + 1, n - 1, acc);
+    else acc = ser_chain_sgpr<T, SG>(in + 1, out + 1, n - 1, acc, &prog);
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+      cyc[0] = t1 - t0;
+      *(volatile size_t *)&prog = ~(size_t)0;  // the prefetch wave's exit, whatever it has requested
+    }
+  } else if (pf) {
+    ser_prefetch(in + 1, (n - 1) * sizeof(T), sizeof(T), &prog, l2a, ka);
+  }
+}
+
 }  // namespace
 
 extern "C" int mc_lab_chain64(const double *init, double *out, long long *cyc, int n, int reps, int kind,
@@ -618,5 +782,43 @@ extern "C" int mc_lab_chain_g(const float *init, float *out, long long *cyc, int
     case 25: k_lab_chain_sgpr<25><<<1, 64, 0, st>>>(init, out, cyc, n, reps, gin, gout); break;
     default: return MC_EINVAL;
   }
+  return mc_last_launch();
+}
+
+// in / out: n elements (kind 0 f32, kind 1 f64); sg selects the group size
+extern "C" int mc_lab_stream(const void *in, void *out, size_t n, int kind, int sg, size_t l2a, size_t ka, int pf,
+                             long long *cyc, mc_stream_t stream) {
+  if (n < 2) return MC_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const float *fi = (const float *)in;
+  float *fo = (float *)out;
+  const double *di = (const double *)in;
+  double *dout = (double *)out;
+#define LS(T, G, I, O) k_lab_stream<T, G><<<1, 128, 0, st>>>(I, O, n, l2a, ka, pf, cyc)
+  if (kind == 0 && sg == 32) LS(float, 32, fi, fo);
+  else if (kind == 0 && sg == 40) LS(float, 40, fi, fo);
+  else if (kind == 0 && sg == 48) LS(float, 48, fi, fo);
+  else if (kind == 0 && sg == 24) LS(float, 24, fi, fo);
+  else if (kind == 1 && sg == 16) LS(double, 16, di, dout);
+  else if (kind == 1 && sg == 20) LS(double, 20, di, dout);
+  else if (kind == 1 && sg == 24) LS(double, 24, di, dout);
+  else if (kind == 1 && sg == 12) LS(double, 12, di, dout);
+  else if (kind >= 2) {
+    const size_t d = ka;
+    ka = 0;
+    if ((uintptr_t)in % 16 != (uintptr_t)out % 16) return MC_EINVAL;
+#define LV(T, G, V, I, O) k_lab_stream<T, G, V><<<1, 128, 0, st>>>(I, O, n, l2a, ka, pf, cyc)
+    if (kind == 2 && sg == 32 && d == 6) LV(float, 32, 6, fi, fo);
+    else if (kind == 2 && sg == 32 && d == 4) LV(float, 32, 4, fi, fo);
+    else if (kind == 2 && sg == 24 && d == 8) LV(float, 24, 8, fi, fo);
+    else if (kind == 2 && sg == 16 && d == 12) LV(float, 16, 12, fi, fo);
+    else if (kind == 3 && sg == 16 && d == 6) LV(double, 16, 6, di, dout);
+    else if (kind == 3 && sg == 12 && d == 8) LV(double, 12, 8, di, dout);
+    else if (kind == 3 && sg == 8 && d == 12) LV(double, 8, 12, di, dout);
+    else return MC_EINVAL;
+#undef LV
+#undef LV
+  } else return MC_EINVAL;
+#undef LS
   return mc_last_launch();
 }

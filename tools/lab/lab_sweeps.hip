@@ -53,7 +53,7 @@ static int lab_grid_cap(int max_blocks) {
 
 int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t elementsize, int encode,
                            int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  if (variant < 0 || (variant & ~0x3FF) != 0) return MC_EINVAL;
   max_blocks = lab_grid_cap(max_blocks);
   return mc_shuffle_impl(src, 0, dst, 0, 1, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
                          (hipStream_t)stream);
@@ -63,7 +63,7 @@ int mc_lab_shuffle_variant(const void *src, void *dst, size_t nbytes, size_t ele
 // layout, as mc_lab_shuffle_variant
 int mc_lab_shuffle_batch_variant(const void *src, size_t ss, void *dst, size_t ds, size_t nchunks, size_t nbytes,
                                  size_t elementsize, int encode, int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  if (variant < 0 || (variant & ~0x3FF) != 0) return MC_EINVAL;
   max_blocks = lab_grid_cap(max_blocks);
   return mc_shuffle_impl(src, ss, dst, ds, nchunks, nbytes, elementsize, encode != 0, variant, max_blocks, nullptr,
                          (hipStream_t)stream);
@@ -73,7 +73,7 @@ int mc_lab_shuffle_batch_variant(const void *src, size_t ss, void *dst, size_t d
 // explicit layout, as mc_lab_shuffle_variant.
 int mc_lab_bitround_shuffle_variant(const void *src, void *dst, size_t n, int itemsize, int keepbits,
                                     int variant, int max_blocks, mc_stream_t stream) {
-  if (variant < 0 || (variant & 7) > 6 || (variant & ~0x3FF) != 0) return MC_EINVAL;
+  if (variant < 0 || (variant & ~0x3FF) != 0) return MC_EINVAL;
   if (!(itemsize == 2 || itemsize == 4 || itemsize == 8)) return MC_EINVAL;
   const int mbits = itemsize == 2 ? 10 : itemsize == 4 ? 23 : 52;
   if (keepbits < 0 || keepbits >= mbits) return MC_EINVAL;

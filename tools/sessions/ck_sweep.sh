@@ -1,5 +1,5 @@
 # the MCODEC_* schedule variables act on the lab library only (tools/lab/lab_sched.hip)
-export NUMCODECS_AMD_LIB="$(cd "$(dirname "$0")" && pwd)/_build/libmcodec_lab.so"
+export NUMCODECS_AMD_LIB="$(cd "$(dirname "$0")/.." && pwd)/_build/libmcodec_lab.so"
 set -u
 cd "${GRAFT_REPO_ROOT}"
 timeout -k 10 600 python -m pytest tests/test_gpu_next.py -q -m gpu -x -p no:cacheprovider > gpurun_out/next.log 2>&1 || { echo "tests failed"; tail -20 gpurun_out/next.log; exit 1; }

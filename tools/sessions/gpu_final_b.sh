@@ -2,7 +2,7 @@
 # round-end refresh, part B: headline rocprof, public-API table, walker
 # families, verify overhead, the driver-contract bench
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o bench -- python3 bench.py --no-cpu --quick --steps 50 --warmup 5 > gpurun_out/rocprof_headline.log 2>&1 || exit $?
 timeout -k 10 400 python3 tools/probe_all.py > gpurun_out/probe_all_final.jsonl 2> gpurun_out/probe_all_final.err || exit $?

@@ -2,7 +2,7 @@
 # round 4, end of round part A: the whole GPU suite, smoke(), the driver's
 # default bench line, and the headline under rocprofv3 (kernel trace + stats)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -rf > gpurun_out/pytest_gpu_final.log 2>&1; rc=$?; grep -E "^FAILED|passed|failed" gpurun_out/pytest_gpu_final.log | tail -20; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_final.log 2>&1 || { tail -20 gpurun_out/smoke_final.log; exit 1; }

@@ -2,7 +2,7 @@
 # round 4, session c: chain schedule probe (rotating register sets), headline
 # rocprof kernel stats, per-config rocprof passes (first half of the configs)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 python -u tools/probe_chain.py > gpurun_out/probe_chain.log 2>&1 || exit $?
 grep '"round": 2' gpurun_out/probe_chain.log

@@ -2,7 +2,7 @@
 # round 4, session h: same-type Delta encode 4 vs 8 vectors per thread
 # (lab A/B + the schedule check of every alternative against the oracle)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/probe_delta_enc_dv.py > gpurun_out/probe_delta_enc_dv.log 2>&1 || exit $?
 cat gpurun_out/probe_delta_enc_dv.log

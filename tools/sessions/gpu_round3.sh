@@ -4,7 +4,7 @@
 # verify overhead, every codec through its public API.  Each step under its
 # own limit; stops at the first crash / abort / timeout.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 run() {  # name limit cmd...
   local name=$1 limit=$2; shift 2

@@ -4,7 +4,7 @@
 # continue past ordinary test failures.  Usage: tools/gpu_session.sh STEP...
 # where STEP is one of: tests, smoke, bench, benchq, benchprof, pmcall, multi, probe, t1p, p1p, prof1p, verify, rocprof, pmc
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 run() {  # name limit cmd...
   local name=$1 limit=$2; shift 2
