@@ -315,10 +315,165 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__r
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined bit-shuffle for ES = 4 / 8 (round 5).  k_bitshuffle_fast runs one
+// 32 KiB (64 KiB) tile per workgroup in three serial phases -- load, barrier,
+// transpose + store -- and its waves spent 77 % of their cycles parked on the
+// loads (SQ_WAIT_ANY, profiles/r05/bsh_pmc.txt) at ~13 resident waves per CU.
+// Here a persistent grid of workgroups walks the tiles, and each thread's
+// share of tile i + 1 is loaded into registers while tile i is transposed and
+// stored, so the loads' latency hides behind the previous tile's work:
+//   encode: R (tile i+1's 16-B element slots) in flight;  R(i) -> LDS,
+//           barrier, issue R(i+1), own 32 elements from LDS -> transposes ->
+//           plane dwords, barrier;
+//   decode: P (tile i+1's plane dwords) in flight;  P(i) -> transposes ->
+//           LDS, issue P(i+1), barrier, coalesced 16-B element stores from
+//           LDS, barrier.
+// The LDS hand-offs use s_barrier after lgkmcnt(0) only (bf_lds_barrier): a
+// full __syncthreads() fence would also wait for the loads in flight.
+// ---------------------------------------------------------------------------
+MC_DEV void bf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int ES, bool FWD>
+__global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_pipe(const uint8_t *__restrict__ src,
+                                                              uint8_t *__restrict__ dst, size_t blocksize,
+                                                              size_t nfull) {
+  static_assert(ES == 4 || ES == 8, "32x32 transposes for 4- and 8-byte elements");
+  constexpr int SLOTS = 2 * ES;  // 16-B slots per thread
+  __shared__ __attribute__((aligned(16))) mc_u32x4 lds[SLOTS * MC_BLOCK];
+  const size_t E = blocksize / ES, ng = E / 8, pstride = E / 8;
+  const size_t tpb = (ng + BF_GROUPS - 1) / BF_GROUPS;  // tiles per block
+  const size_t ntiles = nfull * tpb;
+  const int t = threadIdx.x;
+  // tile -> (block, first group, groups): full tiles except a block's last
+  auto tile = [&](size_t i, size_t &blk, size_t &gw, int &nthr) {
+    blk = i / tpb;
+    gw = (i - blk * tpb) * BF_GROUPS;
+    const size_t gcount = ng - gw < (size_t)BF_GROUPS ? ng - gw : BF_GROUPS;  // multiple of 4
+    nthr = (int)(gcount / BF_GPT);
+  };
+  size_t i = blockIdx.x;
+  if (i >= ntiles) return;
+  size_t blk, gw;
+  int nthr;
+  tile(i, blk, gw, nthr);
+  if (FWD) {
+    mc_u32x4 R[SLOTS];
+    auto load = [&](size_t b, size_t g, int nt) {
+      const uint8_t *s = src + b * blocksize + g * 8 * ES;
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {
+        const int q = t + k * MC_BLOCK;
+        if (q < nt * SLOTS) R[k] = mc_ld16<true>(s + 16 * (size_t)q);
+      }
+    };
+    load(blk, gw, nthr);
+    for (;;) {
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {
+        const int q = t + k * MC_BLOCK;
+        if (q < nthr * SLOTS) lds[bf_slot<ES>(q / SLOTS, q % SLOTS)] = R[k];
+      }
+      bf_lds_barrier();
+      const size_t ni = i + gridDim.x;
+      size_t nblk = 0, ngw = 0;
+      int nnthr = 0;
+      if (ni < ntiles) {
+        tile(ni, nblk, ngw, nnthr);
+        load(nblk, ngw, nnthr);
+      }
+      if (t < nthr) {
+        uint32_t w[8 * ES];
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) {
+          const mc_u32x4 v = lds[bf_slot<ES>(t, k)];
+          w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+        bf_planes_store<ES>(w, dst + blk * blocksize + gw + BF_GPT * (size_t)t, pstride);
+      }
+      if (ni >= ntiles) return;
+      bf_lds_barrier();  // every thread's LDS reads of tile i are done
+      i = ni; blk = nblk; gw = ngw; nthr = nnthr;
+    }
+  } else {
+    uint32_t P[8 * ES];
+    auto load = [&](size_t b, size_t g, int nt) {
+      if (t >= nt) return;
+      const uint8_t *ps = src + b * blocksize + g + BF_GPT * (size_t)t;
+#pragma unroll
+      for (int p = 0; p < 8 * ES; ++p)
+        P[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)p * pstride));
+    };
+    load(blk, gw, nthr);
+    for (;;) {
+      if (t < nthr) {
+        uint32_t w[8 * ES];
+#pragma unroll
+        for (int h = 0; h < ES / 4; ++h) {
+          uint32_t a[32];
+#pragma unroll
+          for (int p = 0; p < 32; ++p) a[p] = P[32 * h + p];
+          tr32x32(a);
+#pragma unroll
+          for (int e = 0; e < 32; ++e) w[(ES / 4) * e + h] = a[e];
+        }
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k)
+          lds[bf_slot<ES>(t, k)] = mc_u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+      }
+      const size_t ni = i + gridDim.x;
+      size_t nblk = 0, ngw = 0;
+      int nnthr = 0;
+      if (ni < ntiles) {
+        tile(ni, nblk, ngw, nnthr);
+        load(nblk, ngw, nnthr);
+      }
+      bf_lds_barrier();
+      uint8_t *d = dst + blk * blocksize + gw * 8 * ES;
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) {
+        const int q = t + k * MC_BLOCK;
+        if (q < nthr * SLOTS) mc_st16<true>(d + 16 * (size_t)q, lds[bf_slot<ES>(q / SLOTS, q % SLOTS)]);
+      }
+      if (ni >= ntiles) return;
+      bf_lds_barrier();  // the stores' LDS reads are done before the next tile's writes
+      i = ni; blk = nblk; gw = ngw; nthr = nnthr;
+    }
+  }
+}
+
+// persistent grid: workgroups per CU as the LDS image allows (32 KiB for
+// ES = 4, 64 KiB for ES = 8, of 160 KiB)
+inline unsigned bf_pipe_grid(int es, size_t ntiles) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  }
+  const size_t g = (size_t)cus * (es == 8 ? 2 : 4);
+  return (unsigned)(ntiles < g ? ntiles : g);
+}
+
 template <int ES>
 void launch_bitshuffle_fast(const uint8_t *s, uint8_t *d, size_t nfull, size_t blocksize, bool fwd,
                             hipStream_t st) {
   const size_t ng = blocksize / ES / 8;
+#ifndef MC_BF_PIPE
+#define MC_BF_PIPE 1
+#endif
+  if constexpr (ES == 4 || ES == 8) {
+    if (MC_BF_PIPE) {
+      const size_t ntiles = nfull * ((ng + BF_GROUPS - 1) / BF_GROUPS);
+      const unsigned g = bf_pipe_grid(ES, ntiles);
+      if (fwd) k_bitshuffle_pipe<ES, true><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
+      else k_bitshuffle_pipe<ES, false><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
+      return;
+    }
+  }
   const dim3 grid((unsigned)nfull, (unsigned)((ng + BF_GROUPS - 1) / BF_GROUPS));
   if (fwd) k_bitshuffle_fast<ES, true><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);
   else k_bitshuffle_fast<ES, false><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);

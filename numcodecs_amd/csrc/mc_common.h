@@ -40,6 +40,16 @@ MC_DEV uint32_t mc_wave_shr1(uint32_t x, uint32_t fill) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x138, 0xF, 0xF, false);
 }
 
+// a pointer the compiler may keep in SGPRs (the value is wave-uniform)
+template <typename P>
+MC_DEV P *mc_uniform_ptr(P *p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return reinterpret_cast<P *>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
+
 template <bool NT>
 MC_DEV mc_u32x4 mc_ld16(const void *p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const mc_u32x4 *>(p));

@@ -256,15 +256,6 @@ MC_DEV typename SerAcc<D>::T ser_group(typename SerAcc<D>::T acc, typename SerAc
   return acc;
 }
 
-// a pointer the compiler may keep in SGPRs (the value is wave-uniform)
-template <typename P>
-MC_DEV P *mc_uniform_ptr(P *p) {
-  const uint64_t v = (uint64_t)(uintptr_t)p;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return reinterpret_cast<P *>((uintptr_t)(((uint64_t)hi << 32) | lo));
-}
-
 // ---------------------------------------------------------------------------
 // The chain fed through VGPRs by uniform-address vector loads (round 5): every
 // lane of the calling wave loads the same 16 B per instruction, runs the same
