@@ -120,9 +120,12 @@ def delta_chunks(chunks, delta, encode=True, out=None):
         # the running sums of every row in `loop`, then one cast of them all
         if b and n:
             sums = delta_chunks(rows, Delta(dtype=loop, astype=delta.astype), encode=False)
-            cast = torch.empty((b, m), dtype=torch.uint8, device=rows.device)
-            _ops.cast(sums, cast, b * n, loop, delta.dtype)
-            out.copy_(cast)
+            if out.is_contiguous():  # one cast straight into the caller's rows
+                _ops.cast(sums, out, b * n, loop, delta.dtype)
+            else:
+                cast = torch.empty((b, m), dtype=torch.uint8, device=rows.device)
+                _ops.cast(sums, cast, b * n, loop, delta.dtype)
+                out.copy_(cast)
         return out
     if not encode and b and nb >= _LARGE_ROW and rows.data_ptr() % 16 == 0 and \
             rows.stride(0) % 16 == 0 and out.stride(0) % 16 == 0 and out.data_ptr() % 16 == 0:

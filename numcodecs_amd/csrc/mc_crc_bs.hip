@@ -22,7 +22,6 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
     uint32_t *__restrict__ partials, const CrcFin fin, const CkFinish fx) {
   static_assert(KIND != K_ADLER && K >= 4, "bit-sliced folds exist for CRC tiles of 4, 8, 16 vectors");
   __shared__ uint32_t red[2][MC_BLOCK / 64];
-  __shared__ uint32_t is_last;  // FUSED: this block arrived last
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t gx[32];  // g * x^i, g = x^(-128 threadIdx.x)
   gx[0] = crc_consts<KIND>().g[threadIdx.x];
@@ -33,26 +32,21 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
     const size_t c = tile / tiles_per_chunk, t = tile - c * tiles_per_chunk;
     ck_load_tile<K, ALS>(v, src + c * src_stride, t * TB + 16 * (size_t)threadIdx.x, n, (t + 1) * TB <= n);
   };
-  auto copy_tile = [&](const mc_u32x4 (&v)[K], size_t tile) {
+  auto fold = [&](const mc_u32x4 (&v)[K], size_t tile, int par) {
     const size_t c = tile / tiles_per_chunk, t = tile - c * tiles_per_chunk;
     const size_t base = t * TB + 16 * (size_t)threadIdx.x;
-    uint8_t *d = dst + c * dst_stride;
-    if ((t + 1) * TB <= n) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) st_vec<ALD>(d + base + (size_t)k * STEP, v[k]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const size_t pos = base + (size_t)k * STEP;
-        if (pos < n) st_masked<ALD>(d, pos, n, v[k]);
-      }
-    }
-  };
-  // copy_now = false: the payload stores are left to the caller (the fused
-  // kernel's last tile stores after its arrival, see below)
-  auto fold = [&](const mc_u32x4 (&v)[K], size_t tile, int par, bool copy_now) {
     if constexpr (COPY) {
-      if (copy_now) copy_tile(v, tile);
+      uint8_t *d = dst + c * dst_stride;
+      if ((t + 1) * TB <= n) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) st_vec<ALD>(d + base + (size_t)k * STEP, v[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const size_t pos = base + (size_t)k * STEP;
+          if (pos < n) st_masked<ALD>(d, pos, n, v[k]);
+        }
+      }
     }
     const uint32_t acc = crc_fold_bs<KIND, K>(v);
     uint32_t p = 0;  // acc * g: bit (31 - i) of acc selects g * x^i
@@ -70,50 +64,20 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
       else partials[tile] = r;
     }
   };
-  // One launch (FUSED): a block's last tile publishes its partial and
-  // arrives BEFORE it stores that tile's payload copy.  The arrival's
-  // s_waitcnt vmcnt(0) then only waits for loads and for stores issued a
-  // tile earlier; arriving after the last tile's copy made every block drain
-  // its final 16 KiB of stores first (round 4: the fused 256 MiB encode ran
-  // 2-3 us slower than tiles + a finalize launch).  The footer bytes never
-  // overlap the payload, so the finishing block needs no payload store.
-  auto last_tile = [&](const mc_u32x4 (&v)[K], size_t tile, int par) {
-    fold(v, tile, par, false);
-    if (threadIdx.x == 0) {  // thread 0 wrote this block's partials
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      is_last = mc_arrive_last(fx.ticket, gridDim.x);
-    }
-    if constexpr (COPY) copy_tile(v, tile);
-    __syncthreads();
-    if (!is_last) return;
-    ck_finish_chunk<KIND, K, true>(fin, partials, tiles_per_chunk, n, fx.init, fx.out, fx.footer, fx.footer_stride,
-                                   fx.stored, src_stride, fx.stored_out, 0);
-    if (threadIdx.x == 0) {  // thread 0 wrote both verdict words
-      mc_publish_verdict_seq(fx.out, fx.seq);
-      mc_arrivals_reset(fx.ticket);  // left zero for the next launch
-    }
-  };
   mc_u32x4 a[K], b[K];
   size_t tile = blockIdx.x;
   if (tile < total_tiles) load(a, tile);
   while (tile < total_tiles) {
     const size_t t1 = tile + gridDim.x;
     if (t1 < total_tiles) load(b, t1);
-    if (FUSED && t1 >= total_tiles) {
-      last_tile(a, tile, 0);
-      return;
-    }
-    fold(a, tile, 0, true);
+    fold(a, tile, 0);
     if (t1 >= total_tiles) break;
     const size_t t2 = t1 + gridDim.x;
     if (t2 < total_tiles) load(a, t2);
-    if (FUSED && t2 >= total_tiles) {
-      last_tile(b, t1, 1);
-      return;
-    }
-    fold(b, t1, 1, true);
+    fold(b, t1, 1);
     tile = t2;
   }
+  if constexpr (FUSED) ck_fused_tail<KIND, K>(fin, partials, tiles_per_chunk, n, src_stride, fx);
 }
 
 namespace {
