@@ -32,6 +32,8 @@ _SIGS = {
     "mc_lab_chain_g": ([_V, _V, _V, _I, _I, _I, _V, _V, _V], _I),
     "mc_lab_chain64": ([_V, _V, _V, _I, _I, _I, _V, _V, _V], _I),
     "mc_lab_stream": ([_V, _V, _S, _I, _I, _S, _S, _I, _V, _V], _I),
+    "mc_lab_crc": ([_I, _V, _S, _I, _I, _I, ctypes.c_uint, _V, _V], _I),
+    "mc_lab_crc_product": ([_I, _V, _S, _I, ctypes.c_uint, _V, _V], _I),
 }
 _lib = None
 
