@@ -367,6 +367,28 @@ def test_blosc_filters_sizes(device, mode):
             assert torch.equal(bsh.unshuffle(got, ts, bs, mode), xd), (ts, nel, bs, mode)
 
 
+@pytest.mark.parametrize("ts", [4, 8])
+def test_bitshuffle_pipelined_grid(device, ts):
+    """The persistent bit-shuffle kernel for 4- / 8-byte types
+    (mc_blosc.hip k_bitshuffle_pipe): more tiles than workgroups (each
+    workgroup loops, the next tile's loads in flight), a partial last tile in
+    every block (38400-B blocks: 1200 groups of 8 = 1024 + 176), a shorter
+    last block (generic kernel) and a block that is a single partial tile;
+    both directions against the oracle."""
+    from numcodecs_amd import blosc_shuffle as bsh
+    from oracle import blosc
+
+    for nbytes, bs in (((24 << 20) + 12 * ts, 38400), ((6 << 20) + 40 * ts, 32 * ts * 5),
+                       (1 << 20, 1 << 20), (3 * 65536 + 64 * ts, 65536)):
+        raw = RNG.integers(0, 256, nbytes, dtype=np.uint8)
+        xd = torch.from_numpy(raw).to(device)
+        ref = blosc.blosc_filter(raw, ts, bs, 2)
+        got = bsh.shuffle(xd, ts, bs, 2)
+        assert got.cpu().numpy().tobytes() == ref, (ts, nbytes, bs)
+        back = bsh.unshuffle(torch.from_numpy(np.frombuffer(ref, np.uint8).copy()).to(device), ts, bs, 2)
+        assert torch.equal(back, xd), (ts, nbytes, bs)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 def test_blosc_filters_blocksize_none_is_one_block(device, mode):
     """blocksize=None filters the whole buffer as ONE block (for every size,
