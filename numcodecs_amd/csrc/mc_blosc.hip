@@ -210,113 +210,55 @@ MC_DEV void bf_planes_store(const uint32_t (&w)[8 * ES], uint8_t *pd, size_t pst
       __builtin_nontemporal_store(a[p], reinterpret_cast<uint32_t *>(pd + (size_t)(32 * h + p) * pstride));
   }
 }
-// and back (the transpose is an involution): plane dwords loaded half by half
+
+// ES = 1 / 2: per group of 8 elements, byte j of the 8 elements -> u64 ->
+// 8x8 bit transpose -> byte k is plane 8j+k's byte for that group; the
+// thread's 4 groups give one dword of each of its 8*ES planes
 template <int ES>
-MC_DEV void bf_planes_load(const uint8_t *ps, size_t pstride, uint32_t (&w)[8 * ES]) {
+MC_DEV void bf_planes_store_small(const uint32_t (&w)[8 * ES], uint8_t *pd, size_t pstride) {
 #pragma unroll
-  for (int h = 0; h < ES / 4; ++h) {
-    uint32_t a[32];
+  for (int j = 0; j < ES; ++j) {
+    uint64_t T[BF_GPT];
 #pragma unroll
-    for (int p = 0; p < 32; ++p)
-      a[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)(32 * h + p) * pstride));
-    tr32x32(a);
+    for (int g = 0; g < BF_GPT; ++g) {
+      uint64_t x = 0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) w[(ES / 4) * i + h] = a[i];
+      for (int r = 0; r < 8; ++r) x |= (uint64_t)bf_byte<ES>(w, 8 * g + r, j) << (8 * r);
+      T[g] = tr8x8(x);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int g = 0; g < BF_GPT; ++g) o |= (uint32_t)((T[g] >> (8 * k)) & 0xffu) << (8 * g);
+      __builtin_nontemporal_store(o, reinterpret_cast<uint32_t *>(pd + (size_t)(8 * j + k) * pstride));
+    }
   }
 }
-
-template <int ES, bool FWD>
-__global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__restrict__ src,
-                                                              uint8_t *__restrict__ dst,
-                                                              size_t blocksize) {
-  constexpr int SLOTS = 2 * ES;  // 16-B slots per thread
-  __shared__ __attribute__((aligned(16))) mc_u32x4 lds[SLOTS * MC_BLOCK];
-  const size_t E = blocksize / ES, ng = E / 8, pstride = E / 8;
-  const size_t gw = (size_t)blockIdx.y * BF_GROUPS;  // first group of the workgroup
-  if (gw >= ng) return;
-  const size_t gcount = ng - gw < (size_t)BF_GROUPS ? ng - gw : BF_GROUPS;  // multiple of 4
-  const int nthr = (int)(gcount / BF_GPT);
-  const int nslots = nthr * SLOTS;
-  const int t = threadIdx.x;
-  const uint8_t *s = src + (size_t)blockIdx.x * blocksize;
-  uint8_t *d = dst + (size_t)blockIdx.x * blocksize;
-  const size_t ebase = gw * 8 * ES;  // byte offset of the workgroup's elements
-  if (FWD) {
-    for (int q = t; q < nslots; q += MC_BLOCK)
-      lds[bf_slot<ES>(q / SLOTS, q % SLOTS)] = mc_ld16<true>(s + ebase + 16 * (size_t)q);
-    __syncthreads();
-    if (t >= nthr) return;
-    uint32_t w[8 * ES];
+// and back: the thread's 8*ES plane dwords -> its 32 elements' 8*ES dwords
+template <int ES>
+MC_DEV void bf_elems_small(const uint32_t (&pl)[8 * ES], uint32_t (&w)[8 * ES]) {
 #pragma unroll
-    for (int i = 0; i < SLOTS; ++i) {
-      const mc_u32x4 v = lds[bf_slot<ES>(t, i)];
-      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-    }
-    uint8_t *pd = d + gw + BF_GPT * (size_t)t;
-    if constexpr (ES == 4 || ES == 8) {
-      bf_planes_store<ES>(w, pd, pstride);
-      return;
-    }
+  for (int i = 0; i < 8 * ES; ++i) w[i] = 0;
 #pragma unroll
-    for (int j = 0; j < ES; ++j) {
-      uint64_t T[BF_GPT];
+  for (int j = 0; j < ES; ++j) {
 #pragma unroll
-      for (int g = 0; g < BF_GPT; ++g) {
-        uint64_t x = 0;
+    for (int g = 0; g < BF_GPT; ++g) {
+      uint64_t x = 0;  // byte k = plane 8j+k's byte for group g
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x |= (uint64_t)bf_byte<ES>(w, 8 * g + r, j) << (8 * r);
-        T[g] = tr8x8(x);
-      }
+      for (int k = 0; k < 8; ++k) x |= (uint64_t)((pl[8 * j + k] >> (8 * g)) & 0xffu) << (8 * k);
+      x = tr8x8(x);  // byte r = byte j of element 8g+r
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int g = 0; g < BF_GPT; ++g) o |= (uint32_t)((T[g] >> (8 * k)) & 0xffu) << (8 * g);
-        __builtin_nontemporal_store(o, reinterpret_cast<uint32_t *>(pd + (size_t)(8 * j + k) * pstride));
+      for (int r = 0; r < 8; ++r) {
+        const int b = (8 * g + r) * ES + j;
+        w[b >> 2] |= (uint32_t)((x >> (8 * r)) & 0xffu) << (8 * (b & 3));
       }
     }
-  } else {
-    uint32_t w[8 * ES];
-    if (t < nthr) {
-      const uint8_t *ps = s + gw + BF_GPT * (size_t)t;
-      if constexpr (ES == 4 || ES == 8) {
-        bf_planes_load<ES>(ps, pstride, w);
-      } else {
-      uint32_t pl[8 * ES];
-#pragma unroll
-      for (int p = 0; p < 8 * ES; ++p)
-        pl[p] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ps + (size_t)p * pstride));
-
-#pragma unroll
-      for (int i = 0; i < 8 * ES; ++i) w[i] = 0;
-#pragma unroll
-      for (int j = 0; j < ES; ++j) {
-#pragma unroll
-        for (int g = 0; g < BF_GPT; ++g) {
-          uint64_t x = 0;  // byte k = plane 8j+k's byte for group g
-#pragma unroll
-          for (int k = 0; k < 8; ++k) x |= (uint64_t)((pl[8 * j + k] >> (8 * g)) & 0xffu) << (8 * k);
-          x = tr8x8(x);  // byte r = byte j of element 8g+r
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const int b = (8 * g + r) * ES + j;
-            w[b >> 2] |= (uint32_t)((x >> (8 * r)) & 0xffu) << (8 * (b & 3));
-          }
-        }
-      }
-      }
-#pragma unroll
-      for (int i = 0; i < SLOTS; ++i)
-        lds[bf_slot<ES>(t, i)] = mc_u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-    }
-    __syncthreads();
-    for (int q = t; q < nslots; q += MC_BLOCK)
-      mc_st16<true>(d + ebase + 16 * (size_t)q, lds[bf_slot<ES>(q / SLOTS, q % SLOTS)]);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined bit-shuffle for ES = 4 / 8 (round 5).  k_bitshuffle_fast runs one
+// Pipelined bit-shuffle, every fast typesize (round 5).  The round-4 kernel ran one
 // 32 KiB (64 KiB) tile per workgroup in three serial phases -- load, barrier,
 // transpose + store -- and its waves spent 77 % of their cycles parked on the
 // loads (SQ_WAIT_ANY, profiles/r05/bsh_pmc.txt) at ~13 resident waves per CU.
@@ -331,6 +273,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_fast(const uint8_t *__r
 //           LDS, barrier.
 // The LDS hand-offs use s_barrier after lgkmcnt(0) only (bf_lds_barrier): a
 // full __syncthreads() fence would also wait for the loads in flight.
+// 256 MiB, 256 KiB blocks, encode / decode µs (profiles/r05/probe_bshuf_all_*):
+// typesize 1 104 / 107 -> 88 / 96, 2 107 / 105 -> 90 / 96, 4 115 / 108 ->
+// 90 / 89, 8 135 / 100 -> 96 / 95.
 // ---------------------------------------------------------------------------
 MC_DEV void bf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -338,7 +283,6 @@ template <int ES, bool FWD>
 __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_pipe(const uint8_t *__restrict__ src,
                                                               uint8_t *__restrict__ dst, size_t blocksize,
                                                               size_t nfull) {
-  static_assert(ES == 4 || ES == 8, "32x32 transposes for 4- and 8-byte elements");
   constexpr int SLOTS = 2 * ES;  // 16-B slots per thread
   __shared__ __attribute__((aligned(16))) mc_u32x4 lds[SLOTS * MC_BLOCK];
   const size_t E = blocksize / ES, ng = E / 8, pstride = E / 8;
@@ -389,7 +333,9 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_pipe(const uint8_t *__r
           const mc_u32x4 v = lds[bf_slot<ES>(t, k)];
           w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
         }
-        bf_planes_store<ES>(w, dst + blk * blocksize + gw + BF_GPT * (size_t)t, pstride);
+        uint8_t *pd = dst + blk * blocksize + gw + BF_GPT * (size_t)t;
+        if constexpr (ES == 4 || ES == 8) bf_planes_store<ES>(w, pd, pstride);
+        else bf_planes_store_small<ES>(w, pd, pstride);
       }
       if (ni >= ntiles) return;
       bf_lds_barrier();  // every thread's LDS reads of tile i are done
@@ -408,14 +354,18 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_pipe(const uint8_t *__r
     for (;;) {
       if (t < nthr) {
         uint32_t w[8 * ES];
+        if constexpr (ES == 4 || ES == 8) {
 #pragma unroll
-        for (int h = 0; h < ES / 4; ++h) {
-          uint32_t a[32];
+          for (int h = 0; h < ES / 4; ++h) {
+            uint32_t a[32];
 #pragma unroll
-          for (int p = 0; p < 32; ++p) a[p] = P[32 * h + p];
-          tr32x32(a);
+            for (int p = 0; p < 32; ++p) a[p] = P[32 * h + p];
+            tr32x32(a);
 #pragma unroll
-          for (int e = 0; e < 32; ++e) w[(ES / 4) * e + h] = a[e];
+            for (int e = 0; e < 32; ++e) w[(ES / 4) * e + h] = a[e];
+          }
+        } else {
+          bf_elems_small<ES>(P, w);
         }
 #pragma unroll
         for (int k = 0; k < SLOTS; ++k)
@@ -442,8 +392,8 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bitshuffle_pipe(const uint8_t *__r
   }
 }
 
-// persistent grid: workgroups per CU as the LDS image allows (32 KiB for
-// ES = 4, 64 KiB for ES = 8, of 160 KiB)
+// persistent grid: workgroups per CU as the LDS image allows (8 / 16 / 32 /
+// 64 KiB for ES = 1 / 2 / 4 / 8, of 160 KiB; at most 8 of 4 waves)
 inline unsigned bf_pipe_grid(int es, size_t ntiles) {
   static int cus = 0;
   if (cus == 0) {
@@ -454,7 +404,7 @@ inline unsigned bf_pipe_grid(int es, size_t ntiles) {
     else
       cus = 256;
   }
-  const size_t g = (size_t)cus * (es == 8 ? 2 : 4);
+  const size_t g = (size_t)cus * (es == 8 ? 2 : es == 4 ? 4 : 8);
   return (unsigned)(ntiles < g ? ntiles : g);
 }
 
@@ -462,21 +412,10 @@ template <int ES>
 void launch_bitshuffle_fast(const uint8_t *s, uint8_t *d, size_t nfull, size_t blocksize, bool fwd,
                             hipStream_t st) {
   const size_t ng = blocksize / ES / 8;
-#ifndef MC_BF_PIPE
-#define MC_BF_PIPE 1
-#endif
-  if constexpr (ES == 4 || ES == 8) {
-    if (MC_BF_PIPE) {
-      const size_t ntiles = nfull * ((ng + BF_GROUPS - 1) / BF_GROUPS);
-      const unsigned g = bf_pipe_grid(ES, ntiles);
-      if (fwd) k_bitshuffle_pipe<ES, true><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
-      else k_bitshuffle_pipe<ES, false><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
-      return;
-    }
-  }
-  const dim3 grid((unsigned)nfull, (unsigned)((ng + BF_GROUPS - 1) / BF_GROUPS));
-  if (fwd) k_bitshuffle_fast<ES, true><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);
-  else k_bitshuffle_fast<ES, false><<<grid, MC_BLOCK, 0, st>>>(s, d, blocksize);
+  const size_t ntiles = nfull * ((ng + BF_GROUPS - 1) / BF_GROUPS);
+  const unsigned g = bf_pipe_grid(ES, ntiles);
+  if (fwd) k_bitshuffle_pipe<ES, true><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
+  else k_bitshuffle_pipe<ES, false><<<g, MC_BLOCK, 0, st>>>(s, d, blocksize, nfull);
 }
 
 inline int launch_bitshuffle_generic(const uint8_t *s, uint8_t *d, size_t nbytes, size_t typesize,
@@ -540,8 +479,7 @@ int mc_blosc_filter(const void *src, void *dst, size_t nbytes, size_t typesize, 
   const size_t nfull = nbytes / blocksize;
   const bool fast_ts = typesize == 1 || typesize == 2 || typesize == 4 || typesize == 8;
   const bool fast = fast_ts && nfull > 0 && blocksize % (32 * typesize) == 0 &&
-                    ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0 &&
-                    blocksize / typesize / 8 / BF_GROUPS < 65536 && nfull <= 0x7fffffffu;
+                    ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0;
   if (!fast) return launch_bitshuffle_generic(s, d, nbytes, typesize, blocksize, fwd, st);
   switch (typesize) {
     case 1: launch_bitshuffle_fast<1>(s, d, nfull, blocksize, fwd, st); break;

@@ -367,12 +367,12 @@ def test_blosc_filters_sizes(device, mode):
             assert torch.equal(bsh.unshuffle(got, ts, bs, mode), xd), (ts, nel, bs, mode)
 
 
-@pytest.mark.parametrize("ts", [4, 8])
+@pytest.mark.parametrize("ts", [1, 2, 4, 8])
 def test_bitshuffle_pipelined_grid(device, ts):
-    """The persistent bit-shuffle kernel for 4- / 8-byte types
-    (mc_blosc.hip k_bitshuffle_pipe): more tiles than workgroups (each
-    workgroup loops, the next tile's loads in flight), a partial last tile in
-    every block (38400-B blocks: 1200 groups of 8 = 1024 + 176), a shorter
+    """The persistent bit-shuffle kernel (mc_blosc.hip k_bitshuffle_pipe,
+    every fast typesize): more tiles than workgroups (each
+    workgroup loops, the next tile's loads in flight), partial last tiles
+    (38400-B blocks: 1200 groups of 8 = 1024 + 176 for typesize 4), a shorter
     last block (generic kernel) and a block that is a single partial tile;
     both directions against the oracle."""
     from numcodecs_amd import blosc_shuffle as bsh
