@@ -34,8 +34,11 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
   dst += (size_t)blockIdx.y * dst_stride;
   const size_t tile_e0 = (size_t)blockIdx.x * (4 * STEPS * MC_BLOCK);
   const int lane = threadIdx.x & 63;
-  // all steps' loads first (n % 16 == 0: quads are whole)
-  uint64_t x[STEPS][4];
+  // all steps' loads first (n % 16 == 0: quads are whole), with lane 0's
+  // element before its quad (the last of the previous wave's quads, read
+  // from memory) -- loaded in the second loop, each was waited for on its
+  // own: STEPS extra round trips per workgroup (round 5)
+  uint64_t x[STEPS][4], before[STEPS];
 #pragma unroll
   for (int q = 0; q < STEPS; ++q) {
     const size_t e = tile_e0 + (size_t)q * 4 * MC_BLOCK + 4 * (size_t)threadIdx.x;
@@ -45,6 +48,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
 #pragma unroll
       for (int k = 0; k < 4; ++k) x[q][k] = 0;
     }
+    before[q] = lane == 0 && e > 0 && e < p.n ? mc_load_elem(src, e - 1, DS) : 0;
   }
 #pragma unroll
   for (int q = 0; q < STEPS; ++q) {
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_enc(const uint8_t *__restrict__
     // the element before the quad is the last one of lane - 1's quad; lane 0
     // reads it (A is at most 32 bits wide, so differences mod 2^32 suffice)
     int64_t prev = (int64_t)(int32_t)mc_wave_shr1((uint32_t)a[3], 0u);
-    if (lane == 0 && e > 0 && e < p.n) prev = fso_enc<D, A>(mc_load_elem(src, e - 1, DS), p);
+    if (lane == 0 && e > 0 && e < p.n) prev = fso_enc<D, A>(before[q], p);
     if (e >= p.n) continue;
     d[0] = e > 0 ? mc_wrap(a[0] - prev, A) : a[0];
 #pragma unroll
@@ -350,15 +354,26 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_reduce_g(const uint8_t *__restr
   const size_t e0 = t0 * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
   uint32_t acc[2] = {0, 0};
   uint32_t v[2][C4_PER];
+  if ((t0 + 2) * MC_SCAN_TILE <= p.n) {
+    // both tiles in range: the loads unbranched, all in flight together
+    // (bounds-branched, the second tile's waited for the first's, round 5)
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (e0 + h * MC_SCAN_TILE < p.n) load16_deltas<A, ES, false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+    for (int h = 0; h < 2; ++h) load16_deltas<A, ES, false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (e0 + h * MC_SCAN_TILE < p.n) {
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
-    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (e0 + h * MC_SCAN_TILE < p.n) load16_deltas<A, ES, false>(src, p.n, e0 + h * MC_SCAN_TILE, v[h]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (e0 + h * MC_SCAN_TILE < p.n) {
+#pragma unroll
+        for (int k = 0; k < C4_PER; ++k) acc[h] += v[h][k];
+      }
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     acc[0] += __shfl_xor(acc[0], off, 64);
@@ -401,13 +416,34 @@ __global__ __launch_bounds__(MC_BLOCK) void k_c4_apply_g(const uint8_t *__restri
   const size_t tile = blockIdx.x;
   const size_t g = tile / GT, gt0 = g * GT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // prefix pieces first (their loads overlap the data loads below)
-  uint32_t x = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;
-  for (unsigned j = threadIdx.x; j < GT && gt0 + j < tile; j += MC_BLOCK) x += tile_tot[gt0 + j];
+  // the data loads first, then the prefix pieces, all in flight together
+  // (k_dscan_apply_g: a loop-carried prefix sum between them made every
+  // workgroup wait for the prefix words before its data loads issued)
   uint32_t v[C4_PER];
   const size_t e0 = tile * MC_SCAN_TILE + (size_t)threadIdx.x * C4_PER;
-  if (e0 < p.n) {
-    load16_deltas<A, ES, false>(src, p.n, e0, v);
+  const bool in = e0 < p.n;
+  mc_u32x4 pl[ES];
+  if (in) {  // raw plane vectors only: converted after the prefix loads issued
+#pragma unroll
+    for (int b = 0; b < ES; ++b) pl[b] = mc_ld16<false>(src + (size_t)b * p.n + e0);
+  }
+  const uint32_t xg = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;
+  auto tile_tots = [&](unsigned j0) {  // 8 of the group's earlier tile totals per thread
+    uint32_t tt[8], y = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t j = j0 + (size_t)u * MC_BLOCK + threadIdx.x;
+      tt[u] = (j < GT && gt0 + j < tile) ? tile_tot[gt0 + j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y += tt[u];
+    return y;
+  };
+  uint32_t x = tile_tots(0);
+  for (unsigned j0 = 8 * MC_BLOCK; j0 < GT; j0 += 8 * MC_BLOCK) x += tile_tots(j0);
+  x += xg;
+  if (in) {
+    c4_planes_to_deltas<A, ES>(pl, v);
   } else {
 #pragma unroll
     for (int k = 0; k < C4_PER; ++k) v[k] = 0;

@@ -140,15 +140,25 @@ MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, int a,
     // every load first, then the byte swaps / conversions: a swap between
     // the (bounds-branched) loads waited for each load before the next issued
     typename Tr::svec xs[FS_Q];
+    if (t0 + fs_tile<D>() <= n) {
+      // a whole tile in range (every tile but a chunk's last): the FS_Q
+      // vector loads with no branch between them, so they are all in flight
+      // together (bounds-branched, each load was waited for before the next
+      // issued -- four round trips per workgroup, round 5)
 #pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
-      const size_t e0 = fs_elem0<D>(t0, q);
-      if (e0 + W <= n) {
-        xs[q] = *reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S));
-      } else {
+      for (int q = 0; q < FS_Q; ++q)
+        xs[q] = *reinterpret_cast<const typename Tr::svec *>(src + fs_elem0<D>(t0, q) * sizeof(typename Tr::S));
+    } else {
 #pragma unroll
-        for (int e = 0; e < W; ++e)
-          xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
+      for (int q = 0; q < FS_Q; ++q) {
+        const size_t e0 = fs_elem0<D>(t0, q);
+        if (e0 + W <= n) {
+          xs[q] = *reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S));
+        } else {
+#pragma unroll
+          for (int e = 0; e < W; ++e)
+            xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
+        }
       }
     }
 #pragma unroll
@@ -164,6 +174,18 @@ MC_DEV void fs_load(const uint8_t *src, size_t n, size_t t0, int a,
     // thread's 2 float32 per vector, the casts in registers.  The components
     // are copied out before the bit casts: __builtin_bit_cast of an
     // ext_vector component reads component 0 (seen in the gfx950 assembly)
+    if (t0 + fs_tile<D>() <= n) {  // a whole tile: every load in flight together (see above)
+      mc_u32x2 xs[FS_Q];
+#pragma unroll
+      for (int q = 0; q < FS_Q; ++q) xs[q] = mc_ld8<false>(src + fs_elem0<D>(t0, q) * 4);
+#pragma unroll
+      for (int q = 0; q < FS_Q; ++q) {
+        const uint32_t x0 = xs[q].x, x1 = xs[q].y;
+        v[q][0] = (double)__builtin_bit_cast(float, x0);
+        v[q][1] = (double)__builtin_bit_cast(float, x1);
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < FS_Q; ++q) {
       const size_t e0 = fs_elem0<D>(t0, q);
@@ -620,16 +642,23 @@ MC_DEV void fsw_load(const uint8_t *src, size_t n, size_t t0, int a,
   constexpr int W = Tr::W;
   if constexpr (A_ == D) {  // every load first, then the swaps / conversions (see fs_load)
     typename Tr::svec xs[FS_Q];
+    if (t0 + fs_tile<D>() <= n) {  // a whole tile: the loads unbranched, all in flight (see fs_load)
 #pragma unroll
-    for (int q = 0; q < FS_Q; ++q) {
-      const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
-      if (e0 + W <= n) {
-        xs[q] = __builtin_nontemporal_load(
-            reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
-      } else {
+      for (int q = 0; q < FS_Q; ++q)
+        xs[q] = __builtin_nontemporal_load(reinterpret_cast<const typename Tr::svec *>(
+            src + (t0 + (size_t)fsw_li(q, 0, W)) * sizeof(typename Tr::S)));
+    } else {
 #pragma unroll
-        for (int e = 0; e < W; ++e)
-          xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
+      for (int q = 0; q < FS_Q; ++q) {
+        const size_t e0 = t0 + (size_t)fsw_li(q, 0, W);
+        if (e0 + W <= n) {
+          xs[q] = __builtin_nontemporal_load(
+              reinterpret_cast<const typename Tr::svec *>(src + e0 * sizeof(typename Tr::S)));
+        } else {
+#pragma unroll
+          for (int e = 0; e < W; ++e)
+            xs[q][e] = e0 + e < n ? reinterpret_cast<const typename Tr::S *>(src)[e0 + e] : (typename Tr::S)0;
+        }
       }
     }
 #pragma unroll

@@ -588,13 +588,59 @@ __global__ __launch_bounds__(MC_BLOCK) void k_dscan_apply_g(const uint8_t *__res
   const size_t tile = blockIdx.x;
   const size_t g = tile / GT, gt0 = g * GT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t x = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;  // before the data loads
-  for (unsigned j = threadIdx.x; j < GT && gt0 + j < tile; j += MC_BLOCK) x += tile_tot[gt0 + j];
   const size_t ea0 = tile * ds_tile<ES>() + (size_t)threadIdx.x * H;
   const size_t eb0 = tile * ds_tile<ES>() + (size_t)(MC_BLOCK + threadIdx.x) * H;
+  // the tile's data and its prefix words in flight together (one memory
+  // round trip per workgroup): a full tile's two vectors first, with no
+  // branch between them and the prefix loads, then the prefix words in
+  // batches of 8 per thread.  (Loaded in the other order, each behind the
+  // previous one's wait, the workgroup paid three round trips: the apply
+  // pass's waves sat parked 72 % of their cycles, round 5.)
+  const bool full = (tile + 1) * ds_tile<ES>() <= n;
+  mc_u32x4 wa{}, wb{};
+  if (full) {
+    wa = mc_ld16<NT>(src + ea0 * ES);
+    wb = mc_ld16<NT>(src + eb0 * ES);
+  }
+  const uint32_t xg = (wave == 0 && (size_t)lane < g) ? gtot[lane] : 0u;
+  auto tile_tots = [&](unsigned j0) {  // 8 of the group's earlier tile totals per thread
+    uint32_t tt[8], y = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t j = j0 + (size_t)u * MC_BLOCK + threadIdx.x;
+      tt[u] = (j < GT && gt0 + j < tile) ? tile_tot[gt0 + j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y += tt[u];
+    return y;
+  };
+  uint32_t x = tile_tots(0);  // GT <= 2048 (up to 128 Mi tiles): this batch only
+  for (unsigned j0 = 8 * MC_BLOCK; j0 < GT; j0 += 8 * MC_BLOCK) x += tile_tots(j0);
+  x += xg;
   T v[PER];
-  ds_load_half<ES, NT, BE>(src, n, ea0, v, 0);
-  ds_load_half<ES, NT, BE>(src, n, eb0, v, H);
+  if (full) {
+    if constexpr (BE) {
+      wa = mc_bswap_vec<ES>(wa);
+      wb = mc_bswap_vec<ES>(wb);
+    }
+    const uint32_t da[4] = {wa.x, wa.y, wa.z, wa.w}, db[4] = {wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      if constexpr (ES == 1) {
+        v[i] = (da[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        v[H + i] = (db[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      } else if constexpr (ES == 2) {
+        v[i] = (da[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+        v[H + i] = (db[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      } else {
+        v[i] = da[i];
+        v[H + i] = db[i];
+      }
+    }
+  } else {
+    ds_load_half<ES, NT, BE>(src, n, ea0, v, 0);
+    ds_load_half<ES, NT, BE>(src, n, eb0, v, H);
+  }
   T ra = 0, rb = 0;
 #pragma unroll
   for (int i = 0; i < H; ++i) {
