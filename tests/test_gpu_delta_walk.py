@@ -221,3 +221,28 @@ def test_codec_and_batch_api_noisy(device, dt):
         assert dec[k].tobytes() == _oracle_dec(_oracle_enc(xs[k], dt), dt).tobytes()
     one = Delta(dt).decode(Delta(dt).encode(xd[2])).cpu().numpy()
     assert one.tobytes() == _oracle_dec(_oracle_enc(xs[2], dt), dt).tobytes()
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("src_off,dst_off", [(0, 0), (4, 4), (8, 8), (12, 12), (4, 0), (0, 8), (12, 4)])
+def test_serial_chain_buffer_offsets(device, dt, src_off, dst_off):
+    """Noise decoded by the serial chains with the buffers at every 4-B
+    offset: equal offsets modulo 16 take the vector-fed chain
+    (mc_scan.h ser_chain_vbc, for f4) with its unaligned head and tail,
+    unequal ones the LDS-fed chain; both equal numpy's cumsum bit for bit."""
+    es = np.dtype(dt).itemsize
+    if src_off % es or dst_off % es:
+        pytest.skip("element-aligned offsets only")
+    n = 3 * _tile(dt) * 64 + 37  # several walker stretches and a ragged end
+    x = family("randn", n, seed=5).astype(dt)
+    enc = _oracle_enc(x, dt)
+    want = _oracle_dec(enc, dt)
+    dev = torch.device("cuda", 0)
+    sbuf = torch.zeros(n * es + 64, dtype=torch.uint8, device=dev)
+    dbuf = torch.zeros(n * es + 64, dtype=torch.uint8, device=dev)
+    sbuf[src_off:src_off + n * es] = torch.from_numpy(enc.view(np.uint8).copy()).to(dev)
+    src = sbuf[src_off:src_off + n * es]
+    dst = dbuf[dst_off:dst_off + n * es]
+    _ops.delta_decode(src, dst, n, dt, dt)
+    torch.cuda.synchronize()
+    assert dst.cpu().numpy().tobytes() == want.tobytes()
