@@ -250,36 +250,48 @@ __global__ __launch_bounds__(64) void k_jenkins(const uint8_t *__restrict__ src,
     const size_t nb = (L - 1) / 12;  // full mixing blocks ("while length > 12")
     size_t blk = 0;
     if (plen == 0 && ((uintptr_t)s & 15) == 0) {
-      // 16 blocks (192 B = 12 x 16-B loads) per group, the next group's loads
-      // in flight while the current one mixes
+      // 16 blocks (192 B = 12 x 16-B loads) per group in a ring of JR groups:
+      // group g + JR - 1 is loaded while group g mixes.  A group's 16 mixes
+      // (~1100 cycles of dependent ALU work) are shorter than a load's
+      // latency, so one group ahead left the chain waiting on memory: one
+      // 16 MiB chunk 98 -> 73 ms, 2048 x 1 MiB 300 -> 392 GB/s
+      // (tools/probe_jenkins.py).  A second wave prefetching the chunk into
+      // L2 ahead of the chain measured no further gain (74.9 ms): the chain's
+      // ~125 cycles per 12-B block are its dependent mix operations
       constexpr size_t G = 16;
+      constexpr int JR = 4;
       const mc_u32x4 *v4 = reinterpret_cast<const mc_u32x4 *>(s);
       const size_t ng = nb / G;
-      mc_u32x4 cur[12];
-      if (ng) {
+      mc_u32x4 ring[JR][12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) cur[j] = v4[j];
-      }
-      for (size_t gi = 0; gi < ng; ++gi) {
-        mc_u32x4 nxt[12];
-        if (gi + 1 < ng) {
+      for (int r = 0; r + 1 < JR; ++r)
+        if ((size_t)r < ng) {
 #pragma unroll
-          for (int j = 0; j < 12; ++j) nxt[j] = v4[12 * (gi + 1) + j];
+          for (int j = 0; j < 12; ++j) ring[r][j] = v4[12 * r + j];
         }
-        uint32_t q[48];
+      for (size_t gi = 0; gi < ng; gi += JR) {
 #pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          q[4 * j] = cur[j].x; q[4 * j + 1] = cur[j].y; q[4 * j + 2] = cur[j].z; q[4 * j + 3] = cur[j].w;
+        for (int r = 0; r < JR; ++r) {
+          const size_t g = gi + r;
+          if (g >= ng) break;
+          if (g + JR - 1 < ng) {
+#pragma unroll
+            for (int j = 0; j < 12; ++j) ring[(r + JR - 1) % JR][j] = v4[12 * (g + JR - 1) + j];
+          }
+          uint32_t q[48];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) {
+            q[4 * j] = ring[r][j].x; q[4 * j + 1] = ring[r][j].y;
+            q[4 * j + 2] = ring[r][j].z; q[4 * j + 3] = ring[r][j].w;
+          }
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            a += q[3 * k];
+            b += q[3 * k + 1];
+            c += q[3 * k + 2];
+            jmix(a, b, c);
+          }
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          a += q[3 * r];
-          b += q[3 * r + 1];
-          c += q[3 * r + 2];
-          jmix(a, b, c);
-        }
-#pragma unroll
-        for (int j = 0; j < 12; ++j) cur[j] = nxt[j];
       }
       blk = ng * G;
       const uint32_t *w = reinterpret_cast<const uint32_t *>(s);
