@@ -72,16 +72,23 @@ __global__ __launch_bounds__(MC_BLOCK) void k_packbits_blk(const uint8_t *__rest
   const size_t B = (size_t)blockIdx.x * PB_SRC, P = (size_t)blockIdx.x * PB_OUT;
   const int t = threadIdx.x;
   mc_u32x4 v[PB_STEPS];
+  if (B + PB_SRC <= n) {
+    // a whole block in range: the loads unbranched, all in flight together
+    // (bounds-branched, each was waited for before the next issued)
 #pragma unroll
-  for (int k = 0; k < PB_STEPS; ++k) {
-    const size_t pos = B + (size_t)k * MC_BLOCK * 16 + 16 * (size_t)t;
-    if (pos + 16 <= n) {
-      v[k] = mc_ld16<true>(src + pos);
-    } else {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (int j = 0; j < 16; ++j)
-        if (pos + j < n) w[j >> 2] |= (uint32_t)src[pos + j] << (8 * (j & 3));
-      v[k] = mc_u32x4{w[0], w[1], w[2], w[3]};
+    for (int k = 0; k < PB_STEPS; ++k) v[k] = mc_ld16<true>(src + B + (size_t)k * MC_BLOCK * 16 + 16 * (size_t)t);
+  } else {
+#pragma unroll
+    for (int k = 0; k < PB_STEPS; ++k) {
+      const size_t pos = B + (size_t)k * MC_BLOCK * 16 + 16 * (size_t)t;
+      if (pos + 16 <= n) {
+        v[k] = mc_ld16<true>(src + pos);
+      } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 16; ++j)
+          if (pos + j < n) w[j >> 2] |= (uint32_t)src[pos + j] << (8 * (j & 3));
+        v[k] = mc_u32x4{w[0], w[1], w[2], w[3]};
+      }
     }
   }
 #pragma unroll
@@ -157,6 +164,22 @@ __global__ __launch_bounds__(MC_BLOCK) void k_unpackbits_wide(const uint8_t *__r
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t base = ((size_t)blockIdx.x * (MC_BLOCK / 64) + wave) * (1024 * V);
   uint32_t x[V];
+  const size_t last_e = 1 + (base + 1024 * (size_t)V) / 8;  // past the wave's last packed byte pair
+  if (base + 1024 * (size_t)V <= n && (last_e & ~(size_t)3) + 8 <= src_bytes) {
+    // the wave's whole range in bounds: the loads unbranched, all in flight
+    // together (bounds-branched, each was waited for before the next issued)
+    mc_u32x2 w[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const size_t e = 1 + (base + 1024 * (size_t)v + 16 * (size_t)lane) / 8;
+      __builtin_memcpy(&w[v], __builtin_assume_aligned(src + (e & ~(size_t)3), 4), 8);
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const size_t e = 1 + (base + 1024 * (size_t)v + 16 * (size_t)lane) / 8;
+      x[v] = __builtin_amdgcn_alignbyte(w[v].y, w[v].x, (uint32_t)(e & 3));
+    }
+  } else {
 #pragma unroll
   for (int v = 0; v < V; ++v) {  // every load first
     const size_t o = base + 1024 * (size_t)v + 16 * (size_t)lane;
@@ -171,6 +194,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_unpackbits_wide(const uint8_t *__r
     } else {
       x[v] = 0;
     }
+  }
   }
 #pragma unroll
   for (int v = 0; v < V; ++v) {
