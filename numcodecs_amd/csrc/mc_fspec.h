@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
             const S pe = e ? c[q][e - 1] : pvs[q];
             const S r = Tr::store(Tr::step(Tr::val(pe), v[q][e]));
             // non-short-circuit (&): no control flow per element
-            const bool ok = (Tr::bits(c[q][e]) == Tr::bits(r)) & Tr::finite(c[q][e]);
+            const bool ok = (int)(Tr::bits(c[q][e]) == Tr::bits(r)) & (int)Tr::finite(c[q][e]);
             const bool bad = (!ok) & (li > fpos) & (li < cnt) & !(q == 0 && e == 0 && lane == 0);
             bm |= (uint32_t)bad << (q * W + e);
           }
@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
           fp = fsw_sel(wfi != NOFAIL, wfp, fp);
           const int lb = w * QE;
           const S r = Tr::store((w == 0 && first_tile) ? bv : Tr::step(Tr::val(pe), bv));  // out[0] = enc[0]
-          const bool bad = (lb > fpos) & (lb < cnt) & !((Tr::bits(bc) == Tr::bits(r)) & Tr::finite(bc));
+          const bool bad = (lb > fpos) & (lb < cnt) & !((int)(Tr::bits(bc) == Tr::bits(r)) & (int)Tr::finite(bc));
           f = fsw_sel(bad, lb, f);
           fv = fsw_sel(bad, r, fv);
           fp = fsw_sel(bad, bp, fp);
