@@ -687,7 +687,7 @@ MC_DEV void ser_prefetch(const void *in, size_t bytes, size_t es, volatile size_
     }
     if (idle) __builtin_amdgcn_s_sleep(2);
   }
-  __shared__ uint32_t sink;
+  [[maybe_unused]] __shared__ uint32_t sink;
   if (seen == 0x9E3779B9u) sink = seen;
 }
 
