@@ -276,6 +276,10 @@ MC_DEV void bf_elems_small(const uint32_t (&pl)[8 * ES], uint32_t (&w)[8 * ES]) 
 // 256 MiB, 256 KiB blocks, encode / decode µs (profiles/r05/probe_bshuf_all_*):
 // typesize 1 104 / 107 -> 88 / 96, 2 107 / 105 -> 90 / 96, 4 115 / 108 ->
 // 90 / 89, 8 135 / 100 -> 96 / 95.
+// Not faster: an opaque per-tile plane stride (no hoisted SGPR offsets) cut
+// decode to 127 / 181 VGPRs for ES 4 / 8 (from 188 / 255+98 AGPRs, one wave
+// per SIMD), yet ts8 decode stayed at 96 us and ts4 rose 88 -> 92 us
+// (profiles/r05/probe_bshuf_regtrim.jsonl).
 // ---------------------------------------------------------------------------
 MC_DEV void bf_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
