@@ -97,7 +97,19 @@ enum mc_dtype {
   MC_C16 = 13, /* '<c16' complex128: two f8 components */
   MC_TD8 = 14, /* '<m8[unit]' timedelta64: int64 ticks, NaT = INT64_MIN */
   MC_DT8 = 15, /* '<M8[unit]' datetime64: int64 ticks, NaT = INT64_MIN */
-  MC_NDTYPES_EXT = 16
+  /* round 6: numpy's longdouble on x86-64 -- the x87 80-bit extended format
+   * (64-bit significand with explicit integer bit, 15-bit exponent) stored in
+   * 16 bytes, 6 of them padding (written as zero; numpy leaves them as
+   * whatever the output buffer held, so only the 10 value bytes are numpy's).
+   * Every operation is one x87 operation: round to nearest even at 64 bits,
+   * gradual underflow, x87 NaN rules (a QNaN beats an SNaN, else the larger
+   * significand; SNaNs quieted), the "real indefinite" NaN for invalid
+   * operations and for the encodings x87 rejects (unnormals, pseudo-NaNs /
+   * pseudo-infinities); casts as gcc compiles numpy's C casts (fst m32 / m64,
+   * fistp with truncation, float16 through float32). */
+  MC_F16L = 16, /* '<f16' longdouble */
+  MC_C32 = 17,  /* '<c32' clongdouble: two MC_F16L components */
+  MC_NDTYPES_EXT = 18
 };
 
 int mc_abi_version(void);
@@ -256,6 +268,28 @@ int mc_fso_encode_x(const void *src, void *dst, size_t n, int dtype, int t1,
 int mc_fso_decode_x(const void *src, void *dst, size_t n, int astype, int t3,
                     int t4, int dtype, double scale_re, double scale_im,
                     double offset_re, double offset_im, mc_stream_t stream);
+/* FixedScaleOffset with the scalars given as raw bytes (host memory, read
+ * during the call): `offset` / `scale` hold the value numpy computes with, in
+ * the compute dtype t1 / t2 (encode) or scale in t3 / offset in t4 (decode),
+ * native byte order, x_itemsize bytes (16 for MC_F16L, 32 for MC_C32).  Any
+ * dtype code; required when a longdouble value does not fit a double
+ * (fixedscaleoffset.py:83-113 with '<f16' / '<c32'). */
+int mc_fso_encode_raw(const void *src, void *dst, size_t n, int dtype, int t1,
+                      int t2, int astype, const void *offset, const void *scale,
+                      mc_stream_t stream);
+int mc_fso_decode_raw(const void *src, void *dst, size_t n, int astype, int t3,
+                      int t4, int dtype, const void *scale, const void *offset,
+                      mc_stream_t stream);
+/* numpy's calendar datetime64 cast (astype.py:46-58 between datetime64 units
+ * where one side is years or months and the other is not: numpy's
+ * datetimestruct path, datetime.c convert_datetime_to_datetimestruct /
+ * convert_datetimestruct_to_datetime): ticks * src_num in unit src_unit ->
+ * the proleptic Gregorian date -> dst_unit ticks floor-divided by dst_num;
+ * NaT stays NaT.  Units are numpy's NPY_DATETIMEUNIT codes (0 Y, 1 M, 2 W,
+ * 3 D, 4 h, 5 m, 6 s, 7 ms, 8 us, 9 ns, 10 ps, 11 fs, 12 as). */
+int mc_cast_calendar(const void *src, void *dst, size_t n, int from_dtype,
+                     int to_dtype, int src_unit, int64_t src_num, int dst_unit,
+                     int64_t dst_num, mc_stream_t stream);
 
 /* ---- Fletcher32 ------------------------------------------------------- */
 size_t mc_fletcher32_workspace(size_t nbytes);

@@ -54,7 +54,10 @@ DTYPE_CODES.update({">" + k[1:]: v | MC_BIG_ENDIAN for k, v in DTYPE_CODES.items
 # any unit (the codes carry no unit: int64 ticks; unit casts take numpy's
 # conversion factor, see numcodecs_amd._ops.datetime_conversion_factor)
 MC_C8, MC_C16, MC_TD8, MC_DT8 = 12, 13, 14, 15
-EXT_CODES = {"c8": MC_C8, "c16": MC_C16, "m8": MC_TD8, "M8": MC_DT8}
+# round 6: numpy's longdouble / clongdouble ('<f16' / '<c32', the x87 80-bit
+# extended type of x86-64)
+MC_F16L, MC_C32 = 16, 17
+EXT_CODES = {"c8": MC_C8, "c16": MC_C16, "m8": MC_TD8, "M8": MC_DT8, "f16": MC_F16L, "c32": MC_C32}
 
 MC_OK = 0
 MC_EINVAL = -22
@@ -115,6 +118,9 @@ _SIGNATURES = {
     "mc_fso_decode_x": [
         _c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int, _c_double, _c_double, _c_double, _c_double, _c_vp,
     ],
+    "mc_fso_encode_raw": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
+    "mc_fso_decode_raw": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
+    "mc_cast_calendar": [_c_vp, _c_vp, _c_size, _c_int, _c_int, _c_int, _c_i64, _c_int, _c_i64, _c_vp],
     "mc_fletcher32_workspace": [_c_size],
     "mc_fletcher32": [_c_vp, _c_size, _c_vp, _c_vp, _c_size, _c_vp],
     "mc_fletcher32_encode": [_c_vp, _c_vp, _c_size, _c_vp, _c_size, _c_vp],

@@ -22,17 +22,23 @@ from ._native import DTYPE_CODES, MC_ARRIVAL_WORDS, check, lib
 __all__ = ["dtype_code", "stream", "workspace"]
 
 
+# numpy's longdouble is the x87 80-bit extended type stored in 16 bytes on
+# x86-64 Linux (the platform the reference runs on and the kernels restate:
+# csrc/mc_x80.h); anywhere else 'f16' would be another format
+_LONGDOUBLE_X87 = np.dtype(np.longdouble).itemsize == 16 and np.finfo(np.longdouble).nmant == 63
+
+
 def dtype_code(dt) -> int:
-    """mc_dtype code of numpy dtype `dt`: bool/int/uint/float/complex and
-    timedelta64/datetime64 (any unit) of either byte order (a big-endian
-    dtype carries MC_BIG_ENDIAN)."""
+    """mc_dtype code of numpy dtype `dt`: bool/int/uint/float (float16 to
+    longdouble)/complex (to clongdouble) and timedelta64/datetime64 (any
+    unit) of either byte order (a big-endian dtype carries MC_BIG_ENDIAN)."""
     dt = np.dtype(dt)
     code = DTYPE_CODES.get(dt.str)
     if code is not None:
         return code
     key = "m8" if dt.kind == "m" else "M8" if dt.kind == "M" else dt.str[1:]
-    code = _native.EXT_CODES.get(key) if dt.kind in "cmM" else None
-    if code is None:
+    code = _native.EXT_CODES.get(key) if is_ext_dtype(dt) else None
+    if code is None or (key in ("f16", "c32") and not _LONGDOUBLE_X87):
         raise NotImplementedError(
             f"dtype {dt.str!r} is not supported by the numcodecs_amd device kernels "
             "(bool/int/uint/float/complex/timedelta64/datetime64 only)"
@@ -41,8 +47,16 @@ def dtype_code(dt) -> int:
 
 
 def is_ext_dtype(dt) -> bool:
-    """complex, timedelta64 or datetime64: the dtypes computed by mc_ext.hip."""
-    return np.dtype(dt).kind in "cmM"
+    """complex, timedelta64, datetime64 or longdouble: the dtypes computed by
+    mc_ext.hip."""
+    dt = np.dtype(dt)
+    return dt.kind in "cmM" or (dt.kind == "f" and dt.itemsize == 16)
+
+
+def is_longdouble(dt) -> bool:
+    """longdouble or clongdouble (csrc/mc_x80.h arithmetic)."""
+    dt = np.dtype(dt)
+    return (dt.kind == "f" and dt.itemsize == 16) or (dt.kind == "c" and dt.itemsize == 32)
 
 
 # numpy's datetime unit table (datetime.c: NPY_DATETIMEUNIT order and
@@ -107,23 +121,34 @@ def datetime_conversion_factor(src, dst) -> "tuple[int, int]":
     return num // g, den // g
 
 
+def calendar_cast(from_dt, to_dt):
+    """(src_unit, src_num, dst_unit, dst_num) of a datetime64 cast numpy runs
+    through its datetimestruct path (years / months on exactly one side:
+    csrc/mc_cal.h), else None.  numpy's own conversion-factor errors are
+    raised first, as its cast does."""
+    f, t = np.dtype(from_dt), np.dtype(to_dt)
+    if f.kind != "M" or t.kind != "M" or np.datetime_data(f) == np.datetime_data(t):
+        return None
+    (fu, fn), (tu, tn) = np.datetime_data(f), np.datetime_data(t)
+    if "generic" in (fu, tu) or (fu in ("Y", "M")) == (tu in ("Y", "M")):
+        return None
+    datetime_conversion_factor(f, t)  # numpy raises its overflow error here too
+    return _DT_UNITS.index(fu), fn, _DT_UNITS.index(tu), tn
+
+
 def time_cast_factor(from_dt, to_dt) -> "tuple[int, int]":
     """The (num, den) mc_cast_units applies for numpy's astype(from -> to):
     a unit conversion between two timedelta64 or two datetime64 dtypes
     (linear units), (1, 1) otherwise (a timedelta <-> datetime cast keeps the
     ticks, as numpy's does).  Calendar conversions of datetime64 between
-    years/months and the other units are not implemented."""
+    years/months and the other units are calendar_cast()'s."""
     f, t = np.dtype(from_dt), np.dtype(to_dt)
     if f.kind not in "mM" or t.kind != f.kind:
         return 1, 1
     if np.datetime_data(f) == np.datetime_data(t):
         return 1, 1
-    if f.kind == "M":
-        fu, tu = np.datetime_data(f)[0], np.datetime_data(t)[0]
-        if (fu in ("Y", "M")) != (tu in ("Y", "M")) and "generic" not in (fu, tu):
-            raise NotImplementedError(
-                f"calendar datetime64 conversion {f.str!r} -> {t.str!r} is not supported by the numcodecs_amd "
-                "device kernels")
+    if calendar_cast(f, t) is not None:
+        raise ValueError(f"{f.str!r} -> {t.str!r} is a calendar cast (calendar_cast)")
     return datetime_conversion_factor(f, t)
 
 
@@ -375,11 +400,24 @@ def _complex_args(value, dt):
     return f, 0.0, i
 
 
+def _raw_scalar(value, dt):
+    """The scalar as numpy holds it in compute dtype `dt` (native bytes, in a
+    ctypes buffer that lives for the call)."""
+    b = np.asarray(value).astype(np.dtype(dt).newbyteorder("=")).tobytes()
+    return ctypes.create_string_buffer(b, max(len(b), 32))
+
+
 def fso_encode(src, dst, n, dtype, t1, t2, astype, offset_t1, scale_t2) -> None:
     _native.require_device()
     if n == 0:
         return
     with _guard(src):
+        if any(is_longdouble(t) for t in (dtype, t1, t2, astype)):
+            off, sc = _raw_scalar(offset_t1, t1), _raw_scalar(scale_t2, t2)
+            check(lib.mc_fso_encode_raw(src.data_ptr(), dst.data_ptr(), n, dtype_code(dtype), dtype_code(t1),
+                                        dtype_code(t2), dtype_code(astype), ctypes.addressof(off),
+                                        ctypes.addressof(sc), stream(src)), "mc_fso_encode_raw")
+            return
         if any(is_ext_dtype(t) for t in (dtype, t1, t2, astype)):
             ore, oim, oi = _complex_args(offset_t1, t1)
             sre, sim, si = _complex_args(scale_t2, t2)
@@ -399,6 +437,12 @@ def fso_decode(src, dst, n, astype, t3, t4, dtype, scale_t3, offset_t4) -> None:
     if n == 0:
         return
     with _guard(src):
+        if any(is_longdouble(t) for t in (astype, t3, t4, dtype)):
+            sc, off = _raw_scalar(scale_t3, t3), _raw_scalar(offset_t4, t4)
+            check(lib.mc_fso_decode_raw(src.data_ptr(), dst.data_ptr(), n, dtype_code(astype), dtype_code(t3),
+                                        dtype_code(t4), dtype_code(dtype), ctypes.addressof(sc),
+                                        ctypes.addressof(off), stream(src)), "mc_fso_decode_raw")
+            return
         if any(is_ext_dtype(t) for t in (astype, t3, t4, dtype)):
             sre, sim, _ = _complex_args(scale_t3, t3)
             ore, oim, _ = _complex_args(offset_t4, t4)
@@ -427,6 +471,11 @@ def cast(src, dst, n, from_dt, to_dt) -> None:
     if n == 0:
         return
     with _guard(src):
+        cal = calendar_cast(from_dt, to_dt)
+        if cal is not None:
+            check(lib.mc_cast_calendar(src.data_ptr(), dst.data_ptr(), n, dtype_code(from_dt), dtype_code(to_dt),
+                                       *cal, stream(src)), "mc_cast_calendar")
+            return
         if is_ext_dtype(from_dt) or is_ext_dtype(to_dt):
             num, den = time_cast_factor(from_dt, to_dt)
             check(lib.mc_cast_units(src.data_ptr(), dst.data_ptr(), n, dtype_code(from_dt), dtype_code(to_dt),

@@ -35,9 +35,7 @@ def _cast(buf, from_dt, to_dt, out=None):
     dst = empty_like_bytes(n * to_dt.itemsize, src) if direct is None else direct
     if from_dt == to_dt:
         _ops.copy(src.data, dst, src.nbytes)
-    elif _ops.is_ext_dtype(from_dt) or _ops.is_ext_dtype(to_dt):
-        _ops.cast(src.data, dst, n, from_dt, to_dt)
-    else:
+    else:  # _ops.cast routes the extended dtypes and the calendar casts itself
         _ops.cast(src.data, dst, n, from_dt, to_dt)
     if direct is not None:
         return out

@@ -461,10 +461,12 @@ MC_HD uint64_t mc_cvtt_u64(double x) {  // gcc's unsigned sequence (no AVX-512)
 }
 
 // ---------------------------------------------------------------------------
-// extended dtypes (mc_ext.hip): complex64/128, timedelta64, datetime64.  The
-// real entry points route these codes here (C++ linkage).
+// extended dtypes (mc_ext.hip): complex64/128, timedelta64, datetime64,
+// longdouble / clongdouble.  The real entry points route these codes here
+// (C++ linkage).
 // ---------------------------------------------------------------------------
-bool mc_ext_code(int dt);  // a valid MC_C8 / MC_C16 / MC_TD8 / MC_DT8 code (either byte order)
+bool mc_ext_code(int dt);  // a valid MC_C8 / MC_C16 / MC_TD8 / MC_DT8 / MC_F16L / MC_C32 code (either byte order)
+int mc_ext_quantize(const void *src, void *dst, size_t n, int dtype, int astype, double scale, hipStream_t st);
 int mc_ext_delta_encode(const void *src, void *dst, size_t n, int dtype, int astype, hipStream_t st);
 size_t mc_ext_delta_decode_workspace(size_t n, int astype, int dtype);
 int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,

@@ -542,6 +542,9 @@ int mc_fso_decode(const void *src, void *dst, size_t n, int astype, int t3, int 
 
 int mc_quantize(const void *src, void *dst, size_t n, int dtype, int astype, double scale,
                 mc_stream_t stream) {
+  const auto ld = [](int t) { return mc_dt_base(t) == MC_F16L && mc_ext_code(t); };
+  if ((ld(dtype) || mc_is_float(dtype)) && (ld(astype) || mc_is_float(astype)) && (ld(dtype) || ld(astype)))
+    return mc_ext_quantize(src, dst, n, dtype, astype, scale, (hipStream_t)stream);
   if (!mc_is_float(dtype) || !mc_is_float(astype)) return MC_EINVAL;
   const int db = mc_dt_base(dtype);  // the computation's dtype (native)
   MapParams p{dtype, db, db, astype, num_scalar(dtype, scale, 0), McNum{0, 0}};

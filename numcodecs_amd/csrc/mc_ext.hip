@@ -1,5 +1,7 @@
 // mc_ext.hip -- the extended dtypes of the elementwise codecs on gfx950:
-// complex64 / complex128, timedelta64 and datetime64 (round 5).
+// complex64 / complex128, timedelta64 and datetime64 (round 5); longdouble /
+// clongdouble ('<f16' / '<c32', numpy's x87 80-bit extended type: mc_x80.h)
+// and the calendar datetime64 casts (mc_cal.h) (round 6).
 //
 //   mc_cast_units   ndarray.astype (astype.py:46-58) incl. datetime unit casts
 //   mc_fso_*_x      fixedscaleoffset.py:83-113 with complex compute dtypes
@@ -17,13 +19,23 @@
 // mc_num_binop) or one wrap-around int64 op.  These dtypes are off the
 // BASELINE path: the kernels move one element per lane per step
 // (lane-contiguous 8- / 16-B accesses), correctness first.
+#include "mc_cal.h"
 #include "mc_num.h"
+#include "mc_x80.h"
+
+#include <string.h>
 
 namespace {
 
 MC_HD bool x_is_complex(int dt) {
   const int b = mc_dt_base(dt);
-  return b == MC_C8 || b == MC_C16;
+  return b == MC_C8 || b == MC_C16 || b == MC_C32;
+}
+// longdouble (MC_F16L) or clongdouble (MC_C32): computed in mc_x80.h
+MC_HD bool x_is_ld(int dt) { return mc_dt_base(dt) == MC_F16L; }
+MC_HD bool x_is_ldf(int dt) {
+  const int b = mc_dt_base(dt);
+  return b == MC_F16L || b == MC_C32;
 }
 MC_HD bool x_is_time(int dt) {
   const int b = mc_dt_base(dt);
@@ -33,14 +45,16 @@ MC_HD bool x_is_ext(int dt) { return mc_dt_base(dt) >= MC_NDTYPES; }
 // component dtype of a complex code (byte order kept: each component of a
 // '>c8' is a big-endian f4)
 MC_HD int x_comp(int dt) {
-  return (mc_dt_base(dt) == MC_C8 ? MC_F4 : MC_F8) | (dt & MC_BIG_ENDIAN);
+  const int b = mc_dt_base(dt);
+  return (b == MC_C8 ? MC_F4 : b == MC_C16 ? MC_F8 : MC_F16L) | (dt & MC_BIG_ENDIAN);
 }
 // the real dtype a non-complex code computes as: time ticks are int64
 MC_HD int x_real(int dt) { return x_is_time(dt) ? (MC_I8 | (dt & MC_BIG_ENDIAN)) : dt; }
 MC_HD int x_itemsize(int dt) {
   switch (mc_dt_base(dt)) {
     case MC_C8: case MC_TD8: case MC_DT8: return 8;
-    case MC_C16: return 16;
+    case MC_C16: case MC_F16L: return 16;
+    case MC_C32: return 32;
     default: return mc_itemsize(dt);
   }
 }
@@ -53,16 +67,26 @@ static inline bool x_valid(int dt) {
 constexpr int64_t NAT = INT64_MIN;
 
 // a value of any dtype: real part / integer / ticks in `re` (McNum), the
-// imaginary part of a complex in `im`
+// imaginary part of a complex in `im`; a longdouble / clongdouble in `x`,
+// `xi` (the 80-bit values, re / im unused)
 struct McX {
   McNum re;
   double im;
+  X80 x, xi;
 };
 
 MC_HD McX x_make(McNum re, double im = 0.0) {
   McX r;
   r.re = re;
   r.im = im;
+  r.x = x80_zero(0);
+  r.xi = x80_zero(0);
+  return r;
+}
+MC_HD McX x_make_ld(X80 x, X80 xi) {
+  McX r = x_make(mc_num_i(0));
+  r.x = x;
+  r.xi = xi;
   return r;
 }
 
@@ -76,7 +100,43 @@ MC_DEV void x_st(uint8_t *p, size_t byte_off, int size, uint64_t v, bool al) {
   else mc_store_elem_u(p + byte_off, 0, size, v);
 }
 
+// a 16-byte longdouble at p + byte_off ('>f16': all 16 bytes reversed)
+MC_DEV X80 x_ld80(const uint8_t *p, size_t byte_off, bool al, bool swapped) {
+  uint64_t w0, w1;
+  if (al) {
+    w0 = *reinterpret_cast<const uint64_t *>(p + byte_off);
+    w1 = *reinterpret_cast<const uint64_t *>(p + byte_off + 8);
+  } else {
+    w0 = mc_load_elem_u(p + byte_off, 0, 8);
+    w1 = mc_load_elem_u(p + byte_off + 8, 0, 8);
+  }
+  if (swapped) {
+    const uint64_t t = __builtin_bswap64(w1);
+    w1 = __builtin_bswap64(w0);
+    w0 = t;
+  }
+  return x80_from_words(w0, w1);
+}
+MC_DEV void x_st80(uint8_t *p, size_t byte_off, X80 v, bool al, bool swapped) {
+  uint64_t w0 = v.m, w1 = v.se & 0xffffu;  // padding bytes zero
+  if (swapped) {
+    const uint64_t t = __builtin_bswap64(w1);
+    w1 = __builtin_bswap64(w0);
+    w0 = t;
+  }
+  if (al) {
+    *reinterpret_cast<uint64_t *>(p + byte_off) = w0;
+    *reinterpret_cast<uint64_t *>(p + byte_off + 8) = w1;
+  } else {
+    mc_store_elem_u(p + byte_off, 0, 8, w0);
+    mc_store_elem_u(p + byte_off + 8, 0, 8, w1);
+  }
+}
+
 MC_DEV McX x_load(const uint8_t *p, size_t idx, int dt, bool al) {
+  if (x_is_ld(dt)) return x_make_ld(x_ld80(p, idx * 16, al, mc_dt_swapped(dt)), x80_zero(0));
+  if (mc_dt_base(dt) == MC_C32)
+    return x_make_ld(x_ld80(p, idx * 32, al, mc_dt_swapped(dt)), x_ld80(p, idx * 32 + 16, al, mc_dt_swapped(dt)));
   if (x_is_complex(dt)) {
     const int c = x_comp(dt), cs = mc_itemsize(c);
     const size_t o = idx * 2 * (size_t)cs;
@@ -87,6 +147,15 @@ MC_DEV McX x_load(const uint8_t *p, size_t idx, int dt, bool al) {
 }
 
 MC_DEV void x_store(uint8_t *p, size_t idx, int dt, const McX &v, bool al) {
+  if (x_is_ld(dt)) {
+    x_st80(p, idx * 16, v.x, al, mc_dt_swapped(dt));
+    return;
+  }
+  if (mc_dt_base(dt) == MC_C32) {
+    x_st80(p, idx * 32, v.x, al, mc_dt_swapped(dt));
+    x_st80(p, idx * 32 + 16, v.xi, al, mc_dt_swapped(dt));
+    return;
+  }
   if (x_is_complex(dt)) {
     const int c = x_comp(dt), cs = mc_itemsize(c);
     const size_t o = idx * 2 * (size_t)cs;
@@ -105,8 +174,52 @@ MC_DEV int64_t x_scale_ticks(int64_t v, int64_t num, int64_t den) {
   return v < 0 ? (int64_t)((uint64_t)m - (uint64_t)(den - 1)) / den : m / den;
 }
 
+// a value's real / imaginary parts as longdoubles (numpy's cast to
+// longdouble / clongdouble: exact, signalling NaNs quieted)
+MC_DEV void x_to_x80(const McX &v, int from, X80 &re, X80 &im) {
+  const int fb = mc_dt_base(from);
+  im = x80_zero(0);
+  if (fb == MC_F16L || fb == MC_C32) {
+    re = v.x;
+    if (fb == MC_C32) im = v.xi;
+    return;
+  }
+  if (fb == MC_C8 || fb == MC_C16) {
+    const int c = fb == MC_C8 ? MC_F4 : MC_F8;
+    re = x80_from_bits(mc_num_to_bits(v.re, c), c);
+    im = x80_from_bits(mc_num_to_bits(mc_num_f(v.im), c), c);
+    return;
+  }
+  if (fb == MC_TD8 || fb == MC_DT8) {
+    re = x80_from_i64(v.re.i);
+    return;
+  }
+  re = x80_from_bits(mc_num_to_bits(v.re, fb), fb);
+}
+
+// longdouble real / imaginary parts cast to dtype `to` (numpy's casts from
+// longdouble / clongdouble: the imaginary part is dropped for a real `to`)
+MC_DEV McX x_from_x80(X80 re, X80 im, int to) {
+  const int tb = mc_dt_base(to);
+  if (tb == MC_F16L) return x_make_ld(re, x80_zero(0));
+  if (tb == MC_C32) return x_make_ld(re, im);
+  if (tb == MC_B1) return x_make(mc_num_i(x80_nonzero(re) || x80_nonzero(im)));
+  if (tb == MC_C8 || tb == MC_C16) {
+    const int c = tb == MC_C8 ? MC_F4 : MC_F8;
+    return x_make(mc_num_from_bits(x80_to_bits(re, c), c), mc_num_from_bits(x80_to_bits(im, c), c).f);
+  }
+  if (tb == MC_TD8 || tb == MC_DT8) return x_make(mc_num_i(x80_trunc_int(re, 64)));
+  return x_make(mc_num_from_bits(x80_to_bits(re, tb), tb));
+}
+
 // numpy astype(from -> to), unsafe casting
 MC_DEV McX x_cast(const McX &v, int from, int to, int64_t num, int64_t den) {
+  if (x_is_ldf(from) || x_is_ldf(to)) {
+    if (mc_dt_base(from) == mc_dt_base(to)) return v;
+    X80 re, im;
+    x_to_x80(v, from, re, im);
+    return x_from_x80(re, im, to);
+  }
   if (x_is_complex(from)) {
     const int fc = mc_dt_base(x_comp(from));
     if (x_is_complex(to)) {
@@ -123,7 +236,18 @@ MC_DEV McX x_cast(const McX &v, int from, int to, int64_t num, int64_t den) {
 
 // component-wise op of a complex dtype / NaT-aware op of a time dtype / the
 // real op
+MC_DEV X80 x80_op(X80 a, X80 b, int op) {
+  switch (op) {
+    case MC_OP_ADD: return x80_add(a, b);
+    case MC_OP_SUB: return x80_sub(a, b);
+    case MC_OP_MUL: return x80_mul(a, b);
+    default: return x80_div(a, b);
+  }
+}
+
 MC_DEV McX x_addsub(const McX &a, const McX &b, int op, int dt) {
+  if (x_is_ld(dt)) return x_make_ld(x80_op(a.x, b.x, op), x80_zero(0));
+  if (mc_dt_base(dt) == MC_C32) return x_make_ld(x80_op(a.x, b.x, op), x80_op(a.xi, b.xi, op));
   if (x_is_complex(dt)) {
     const int c = mc_dt_base(x_comp(dt));
     return x_make(mc_num_binop(a.re, b.re, op, c), mc_num_binop(mc_num_f(a.im), mc_num_f(b.im), op, c).f);
@@ -141,6 +265,12 @@ MC_DEV double x_op(double a, double b, int op, int c) { return mc_num_binop(mc_n
 MC_DEV double x_fabs(double a) { return __builtin_fabs(a); }
 
 MC_DEV McX x_mul(const McX &a, const McX &b, int dt) {
+  if (x_is_ld(dt)) return x_make_ld(x80_mul(a.x, b.x), x80_zero(0));
+  if (mc_dt_base(dt) == MC_C32) {  // (ar*br - ai*bi, ar*bi + ai*br), each op one x87 op
+    const X80 re = x80_sub(x80_mul(a.x, b.x), x80_mul(a.xi, b.xi));
+    const X80 im = x80_add(x80_mul(a.x, b.xi), x80_mul(a.xi, b.x));
+    return x_make_ld(re, im);
+  }
   if (!x_is_complex(dt)) return x_make(mc_num_binop(a.re, b.re, MC_OP_MUL, dt));
   const int c = mc_dt_base(x_comp(dt));
   const double ar = a.re.f, ai = a.im, br = b.re.f, bi = b.im;
@@ -149,8 +279,50 @@ MC_DEV McX x_mul(const McX &a, const McX &b, int dt) {
   return x_make(mc_num_f(re), im);
 }
 
+// |a| >= |b| for longdoubles (false when either is a NaN or a rejected
+// format, as the x87 compare is unordered)
+MC_DEV bool x80_abs_ge(X80 a, X80 b) {
+  const int ca = x80_class(a), cb = x80_class(b);
+  if (ca == X80_QNAN || ca == X80_SNAN || ca == X80_BAD || cb == X80_QNAN || cb == X80_SNAN || cb == X80_BAD)
+    return false;
+  if (cb == X80_ZERO) return true;
+  if (ca == X80_ZERO) return false;
+  if (ca == X80_INF) return true;
+  if (cb == X80_INF) return false;
+  // normalise (denormals / pseudo-denormals) and compare exponent, significand
+  const int ka = x80_clz64(a.m), kb = x80_clz64(b.m);
+  const int ea = x80_eexp(a) - ka, eb = x80_eexp(b) - kb;
+  if (ea != eb) return ea > eb;
+  return (a.m << ka) >= (b.m << kb);
+}
+MC_DEV X80 x80_abs(X80 a) { return x80_make(a.m, a.se & 0x7fffu); }
+MC_DEV X80 x80_one() { return x80_make(X80_J, X80_BIAS); }
+
 // numpy's complex divide (umath loops.c.src @TYPE@_divide)
 MC_DEV McX x_div(const McX &a, const McX &b, int dt) {
+  if (x_is_ld(dt)) return x_make_ld(x80_div(a.x, b.x), x80_zero(0));
+  if (mc_dt_base(dt) == MC_C32) {
+    const X80 ar = a.x, ai = a.xi, br = b.x, bi = b.xi;
+    const X80 abr = x80_abs(br), abi = x80_abs(bi);
+    X80 re, im;
+    if (x80_abs_ge(abr, abi)) {
+      if (x80_class(abr) == X80_ZERO && x80_class(abi) == X80_ZERO) {
+        re = x80_div(ar, abr);
+        im = x80_div(ai, abr);
+      } else {
+        const X80 rat = x80_div(bi, br);
+        const X80 scl = x80_div(x80_one(), x80_add(br, x80_mul(bi, rat)));
+        re = x80_mul(x80_add(ar, x80_mul(ai, rat)), scl);
+        im = x80_mul(x80_sub(ai, x80_mul(ar, rat)), scl);
+      }
+    } else {
+      const X80 rat = x80_div(br, bi);
+      const X80 scl = x80_div(x80_one(), x80_add(bi, x80_mul(br, rat)));
+      re = x80_mul(x80_add(x80_mul(ar, rat), ai), scl);
+      im = x80_mul(x80_sub(x80_mul(ai, rat), ar), scl);
+    }
+    return x_make_ld(re, im);
+  }
   if (!x_is_complex(dt)) return x_make(mc_num_binop(a.re, b.re, MC_OP_DIV, dt));
   const int c = mc_dt_base(x_comp(dt));
   const double ar = a.re.f, ai = a.im, br = b.re.f, bi = b.im;
@@ -176,17 +348,21 @@ MC_DEV McX x_div(const McX &a, const McX &b, int dt) {
 }
 
 MC_DEV McX x_rint(const McX &v, int dt) {
+  if (x_is_ld(dt)) return x_make_ld(x80_rint(v.x), x80_zero(0));
+  if (mc_dt_base(dt) == MC_C32) return x_make_ld(x80_rint(v.x), x80_rint(v.xi));
   if (!x_is_complex(dt)) return x_make(mc_num_rint(v.re, dt));
   const int c = mc_dt_base(x_comp(dt));
   return x_make(mc_num_rint(v.re, c), mc_num_rint(mc_num_f(v.im), c).f);
 }
 
-enum XKind { X_CAST = 0, X_FSO_ENC = 1, X_FSO_DEC = 2 };
+enum XKind { X_CAST = 0, X_FSO_ENC = 1, X_FSO_DEC = 2, X_QUANT = 3, X_CAL = 4 };
 
 struct XParams {
   int d, t1, t2, a;  // input dtype, compute dtypes, output dtype
   McX s0, s1;        // scalars in their compute dtypes
   int64_t num, den;  // unit conversion (X_CAST between time dtypes)
+  int su, du;        // X_CAL: numpy datetime units and multipliers
+  int64_t sn, dn;
   bool al;           // both buffers aligned to their component sizes
 };
 
@@ -203,6 +379,14 @@ __global__ __launch_bounds__(MC_BLOCK) void k_xmap(const uint8_t *__restrict__ s
     McX v = x_load(src, i, p.d, p.al);
     if constexpr (KIND == X_CAST) {
       v = x_cast(v, p.d, p.a, p.num, p.den);
+    } else if constexpr (KIND == X_CAL) {  // datetime64 -> datetime64 through the calendar date
+      v = x_make(mc_num_i(mc_cal_convert(v.re.i, p.su, p.sn, p.du, p.dn)));
+    } else if constexpr (KIND == X_QUANT) {  // astype(rint(scale * x) / scale), in dtype t1
+      v = x_cast(v, p.d, p.t1, 1, 1);
+      v = x_mul(p.s0, v, p.t1);
+      v = x_rint(v, p.t1);
+      v = x_div(v, p.s0, p.t1);
+      v = x_cast(v, p.t1, p.a, 1, 1);
     } else if constexpr (KIND == X_FSO_ENC) {  // astype(rint((x - offset) * scale))
       v = x_cast(v, p.d, p.t1, 1, 1);
       v = x_addsub(v, p.s0, MC_OP_SUB, p.t1);
@@ -243,6 +427,15 @@ __global__ __launch_bounds__(MC_BLOCK) void k_xdelta_enc(const uint8_t *__restri
 __global__ __launch_bounds__(MC_BLOCK) void k_xsplit(const uint8_t *__restrict__ src, uint8_t *__restrict__ re,
                                                     uint8_t *__restrict__ im, size_t n, int dt, bool al) {
   const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  if (mc_dt_base(dt) == MC_C32) {  // 16-B longdouble components, little-endian planes
+    for (int s = 0; s < X_STEPS; ++s) {
+      const size_t i = base + (size_t)s * MC_BLOCK;
+      if (i >= n) return;
+      x_st80(re, i * 16, x_ld80(src, i * 32, al, mc_dt_swapped(dt)), true, false);
+      x_st80(im, i * 16, x_ld80(src, i * 32 + 16, al, mc_dt_swapped(dt)), true, false);
+    }
+    return;
+  }
   const int c = x_comp(dt), cs = mc_itemsize(c);
 #pragma unroll
   for (int s = 0; s < X_STEPS; ++s) {
@@ -261,6 +454,15 @@ __global__ __launch_bounds__(MC_BLOCK) void k_xmerge(const uint8_t *__restrict__
                                                     uint8_t *__restrict__ dst, size_t n, int lc, int dt,
                                                     bool al) {
   const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+  if (lc == MC_F16L) {  // longdouble planes: the clongdouble sums, cast to dtype
+    for (int s = 0; s < X_STEPS; ++s) {
+      const size_t i = base + (size_t)s * MC_BLOCK;
+      if (i >= n) return;
+      const McX v = x_make_ld(x_ld80(re, i * 16, true, false), im ? x_ld80(im, i * 16, true, false) : x80_zero(0));
+      x_store(dst, i, dt, x_cast(v, MC_C32, dt, 1, 1), al);
+    }
+    return;
+  }
   const int loop = lc == MC_F4 ? MC_C8 : MC_C16;
   const int cs = mc_itemsize(lc);
   // the same component type: the sums' bits moved as they are (a signalling
@@ -484,10 +686,72 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bswap(const uint8_t *__restrict__ 
   }
 }
 
+// byte reversal of n 16-byte elements ('<f16' <-> '>f16', '<c32' components)
+__global__ __launch_bounds__(MC_BLOCK) void k_bswap16(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                     size_t n, bool al) {
+  const size_t base = (size_t)blockIdx.x * X_STEPS * MC_BLOCK + threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < X_STEPS; ++s) {
+    const size_t i = base + (size_t)s * MC_BLOCK;
+    if (i >= n) return;
+    uint64_t w0, w1;
+    if (al) {
+      w0 = reinterpret_cast<const uint64_t *>(src)[2 * i];
+      w1 = reinterpret_cast<const uint64_t *>(src)[2 * i + 1];
+    } else {
+      w0 = mc_load_elem_u(src + 16 * i, 0, 8);
+      w1 = mc_load_elem_u(src + 16 * i + 8, 0, 8);
+    }
+    const uint64_t r0 = __builtin_bswap64(w1), r1 = __builtin_bswap64(w0);
+    if (al) {
+      reinterpret_cast<uint64_t *>(dst)[2 * i] = r0;
+      reinterpret_cast<uint64_t *>(dst)[2 * i + 1] = r1;
+    } else {
+      mc_store_elem_u(dst + 16 * i, 0, 8, r0);
+      mc_store_elem_u(dst + 16 * i + 8, 0, 8, r1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Delta decode with a longdouble loop (np.cumsum(enc, out=dec) accumulates in
+// promote(astype, dtype) = longdouble when either side is '<f16', delta.py:80):
+// one x87 add per element in numpy's left-to-right order, one workgroup.
+// Each batch of LDC_N elements is cast to longdouble by all threads into LDS,
+// thread 0 runs the chain over it, and all threads cast the running sums to
+// dtype and store them.  The first sum is the first element itself (numpy's
+// accumulate copies it).
+// ---------------------------------------------------------------------------
+constexpr int LDC_N = 4 * MC_BLOCK;
+
+__global__ __launch_bounds__(MC_BLOCK) void k_ld_chain(const uint8_t *__restrict__ src, int a,
+                                                      uint8_t *__restrict__ dst, int d, size_t n, bool al) {
+  __shared__ X80 buf[LDC_N];
+  X80 sum = x80_zero(0);
+  for (size_t b0 = 0; b0 < n; b0 += LDC_N) {
+    const int cnt = (int)(n - b0 < (size_t)LDC_N ? n - b0 : (size_t)LDC_N);
+    for (int j = threadIdx.x; j < cnt; j += MC_BLOCK) {
+      X80 re, im;
+      x_to_x80(x_load(src, b0 + j, a, al), a, re, im);
+      buf[j] = re;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < cnt; ++j) {
+        sum = (b0 == 0 && j == 0) ? buf[j] : x80_add(sum, buf[j]);
+        buf[j] = sum;
+      }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < cnt; j += MC_BLOCK) x_store(dst, b0 + j, d, x_from_x80(buf[j], x80_zero(0), d), al);
+    __syncthreads();
+  }
+}
+
 unsigned x_grid(size_t n) { return (unsigned)((n + (size_t)X_STEPS * MC_BLOCK - 1) / ((size_t)X_STEPS * MC_BLOCK)); }
 
 bool x_aligned(const void *p, int dt) {
-  const int cs = x_is_complex(dt) ? mc_itemsize(x_comp(dt)) : x_itemsize(dt);
+  const int cs = x_is_complex(dt) ? x_itemsize(x_comp(dt)) : x_itemsize(dt);
   return (uintptr_t)p % (uintptr_t)cs == 0;
 }
 
@@ -515,11 +779,12 @@ int x_promote_comp(int astype, int dtype) {
     switch (mc_dt_base(dt)) {
       case MC_C8: case MC_F4: case MC_I2: case MC_U2: return 4;
       case MC_C16: case MC_F8: case MC_I4: case MC_U4: case MC_I8: case MC_U8: return 8;
+      case MC_C32: case MC_F16L: return 16;
       default: return 2;  // b1, i1, u1, f2
     }
   };
   const int w = need(astype) > need(dtype) ? need(astype) : need(dtype);
-  return w == 8 ? MC_F8 : MC_F4;
+  return w == 16 ? MC_F16L : w == 8 ? MC_F8 : MC_F4;
 }
 
 }  // namespace
@@ -540,6 +805,8 @@ int mc_ext_bswap(const void *src, void *dst, size_t n, int es, hipStream_t st) {
     case 2: k_bswap<2><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
     case 4: k_bswap<4><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
     case 8: k_bswap<8><<<g, MC_BLOCK, 0, st>>>(s, d, nbytes, vec); break;
+    case 16: k_bswap16<<<x_grid(n), MC_BLOCK, 0, st>>>(s, d, n, (uintptr_t)src % 8 == 0 && (uintptr_t)dst % 8 == 0);
+      break;
     default: return MC_EINVAL;
   }
   return mc_last_launch();
@@ -569,6 +836,11 @@ static bool cx_pair(int astype, int dtype) {
   if (!x_is_complex(astype) && !x_is_complex(dtype)) return false;
   return !x_is_time(astype) && !x_is_time(dtype);
 }
+// a real pair whose loop dtype is longdouble
+static bool ld_pair(int astype, int dtype) {
+  if (x_is_complex(astype) || x_is_complex(dtype) || x_is_time(astype) || x_is_time(dtype)) return false;
+  return x_is_ld(astype) || x_is_ld(dtype);
+}
 
 static int nanfix(const uint8_t *in, int ac, uint8_t *out, int lc, size_t n, long long *last, long long *carry,
                   hipStream_t st) {
@@ -589,8 +861,8 @@ size_t mc_ext_delta_decode_workspace(size_t n, int astype, int dtype) {
   if (cx_pair(astype, dtype)) {
     const int lc = x_promote_comp(astype, dtype);
     const int ac = x_is_complex(astype) ? mc_dt_base(x_comp(astype)) : mc_dt_base(astype);
-    const size_t in_planes = x_is_complex(astype) ? 2 * x_align_up(n * mc_itemsize(ac)) : 0;
-    const size_t out_planes = 2 * x_align_up(n * mc_itemsize(lc));
+    const size_t in_planes = x_is_complex(astype) ? 2 * x_align_up(n * x_itemsize(ac)) : 0;
+    const size_t out_planes = 2 * x_align_up(n * x_itemsize(lc));
     const size_t nf = 2 * ((n + NF_BLOCK - 1) / NF_BLOCK) * sizeof(long long);  // NaN-fix blocks
     const size_t rw = mc_delta_decode_workspace(n, ac, lc);
     return in_planes + out_planes + (rw > nf ? rw : nf);
@@ -601,6 +873,13 @@ size_t mc_ext_delta_decode_workspace(size_t n, int astype, int dtype) {
 int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype, void *workspace,
                         size_t workspace_bytes, uint32_t *ticket, hipStream_t st) {
   if (!x_valid(dtype) || !x_valid(astype)) return MC_EINVAL;
+  if (ld_pair(astype, dtype)) {  // no workspace
+    if (n == 0) return MC_OK;
+    if (!src || !dst) return MC_EINVAL;
+    k_ld_chain<<<1, MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), astype, static_cast<uint8_t *>(dst), dtype,
+                                       n, x_aligned(src, astype) && x_aligned(dst, dtype));
+    return mc_last_launch();
+  }
   const bool td = td_pair(astype, dtype), cx = cx_pair(astype, dtype);
   if (!td && !cx) return MC_EINVAL;
   if (n == 0) return MC_OK;
@@ -628,12 +907,12 @@ int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dt
   // complex: per component, the running sums in the loop's component type lc
   const int lc = x_promote_comp(astype, dtype);
   const int ac = x_is_complex(astype) ? mc_dt_base(x_comp(astype)) : astype;
-  const size_t lcs = mc_itemsize(lc);
+  const size_t lcs = x_itemsize(lc);
   size_t off = 0;
   const uint8_t *in_re = static_cast<const uint8_t *>(src), *in_im = nullptr;
   if (x_is_complex(astype)) {
-    uint8_t *pre = ws + off, *pim = ws + off + x_align_up(n * mc_itemsize(ac));
-    off += 2 * x_align_up(n * mc_itemsize(ac));
+    uint8_t *pre = ws + off, *pim = ws + off + x_align_up(n * x_itemsize(ac));
+    off += 2 * x_align_up(n * x_itemsize(ac));
     k_xsplit<<<x_grid(n), MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), pre, pim, n, astype,
                                              x_aligned(src, astype));
     int rc = mc_last_launch();
@@ -646,7 +925,8 @@ int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dt
   uint8_t *rws = ws + off;
   const size_t rws_bytes = workspace_bytes - off;
   // numpy's NaN + NaN operand choice of the complex loop (see k_nanfix_*)
-  const bool second = (lc == MC_F4) != (n == 2);
+  // (clongdouble adds are x87 adds, whose NaN choice the real chain makes)
+  const bool second = lc != MC_F16L && ((lc == MC_F4) != (n == 2));
   const size_t nb = (n + NF_BLOCK - 1) / NF_BLOCK;
   long long *nf_last = reinterpret_cast<long long *>(rws), *nf_carry = nf_last + nb;
   int rc = mc_delta_decode(in_re, out_re, n, ac, lc, rws, rws_bytes, nullptr, st);
@@ -663,7 +943,8 @@ int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dt
 }
 
 static int mc_ext_map(int kind, const void *src, void *dst, size_t n, int d, int t1, int t2, int a, McX s0, McX s1,
-               int64_t num, int64_t den, hipStream_t st) {
+                      int64_t num, int64_t den, hipStream_t st, int su = 0, int64_t sn = 1, int du = 0,
+                      int64_t dn = 1) {
   if (!x_valid(d) || !x_valid(a) || !x_valid(t1) || !x_valid(t2)) return MC_EINVAL;
   if (mc_dt_swapped(t1) || mc_dt_swapped(t2)) return MC_EINVAL;
   if (num <= 0 || den <= 0) return MC_EINVAL;
@@ -678,18 +959,102 @@ static int mc_ext_map(int kind, const void *src, void *dst, size_t n, int d, int
   p.s1 = s1;
   p.num = num;
   p.den = den;
+  p.su = su;
+  p.sn = sn;
+  p.du = du;
+  p.dn = dn;
   p.al = x_aligned(src, d) && x_aligned(dst, a);
   const uint8_t *s = static_cast<const uint8_t *>(src);
   uint8_t *o = static_cast<uint8_t *>(dst);
   switch (kind) {
     case X_CAST: k_xmap<X_CAST><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
     case X_FSO_ENC: k_xmap<X_FSO_ENC><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
+    case X_QUANT: k_xmap<X_QUANT><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
+    case X_CAL: k_xmap<X_CAL><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
     default: k_xmap<X_FSO_DEC><<<x_grid(n), MC_BLOCK, 0, st>>>(s, o, n, p); break;
   }
   return mc_last_launch();
 }
 
+// scalar of dtype dt from its raw native bytes (host memory)
+static McX x_from_raw(const void *p, int dt) {
+  const uint8_t *b = static_cast<const uint8_t *>(p);
+  auto u = [&](int off, int size) {
+    uint64_t v = 0;
+    for (int k = 0; k < size; ++k) v |= (uint64_t)b[off + k] << (8 * k);
+    return v;
+  };
+  auto fbits = [&](uint64_t bits, int c) -> double {  // float component value (exact in a double)
+    if (c == MC_F8) {
+      double d;
+      memcpy(&d, &bits, 8);
+      return d;
+    }
+    const uint32_t f32 = c == MC_F4 ? (uint32_t)bits : mc_half_to_float_bits((uint16_t)bits);
+    float f;
+    memcpy(&f, &f32, 4);
+    return (double)f;
+  };
+  const int base = mc_dt_base(dt);
+  switch (base) {
+    case MC_F16L: return x_make_ld(x80_from_words(u(0, 8), u(8, 8)), x80_zero(0));
+    case MC_C32: return x_make_ld(x80_from_words(u(0, 8), u(8, 8)), x80_from_words(u(16, 8), u(24, 8)));
+    case MC_C8: return x_make(mc_num_f(fbits(u(0, 4), MC_F4)), fbits(u(4, 4), MC_F4));
+    case MC_C16: return x_make(mc_num_f(fbits(u(0, 8), MC_F8)), fbits(u(8, 8), MC_F8));
+    case MC_F2: case MC_F4: case MC_F8: return x_make(mc_num_f(fbits(u(0, x_itemsize(base)), base)));
+    case MC_B1: return x_make(mc_num_i(b[0] != 0));
+    case MC_I1: return x_make(mc_num_i((int8_t)u(0, 1)));
+    case MC_I2: return x_make(mc_num_i((int16_t)u(0, 2)));
+    case MC_I4: return x_make(mc_num_i((int32_t)u(0, 4)));
+    case MC_U1: case MC_U2: case MC_U4: return x_make(mc_num_i((int64_t)u(0, x_itemsize(base))));
+    default: return x_make(mc_num_i((int64_t)u(0, 8)));  // i8, u8 (bit pattern), time ticks
+  }
+}
+
+// Quantize encode with an extended dtype (mc_quantize routes here): the
+// power-of-two scale is exact in every float dtype numpy converts it to
+int mc_ext_quantize(const void *src, void *dst, size_t n, int dtype, int astype, double scale, hipStream_t st) {
+  const int t = mc_dt_base(dtype);
+  McX s0 = x_make(mc_num_f(scale));
+  if (t == MC_F16L) {
+    uint64_t bits;
+    memcpy(&bits, &scale, 8);
+    s0 = x_make_ld(x80_from_f64_bits(bits), x80_zero(0));
+  }
+  return mc_ext_map(X_QUANT, src, dst, n, dtype, t, t, astype, s0, x_make(mc_num_i(0)), 1, 1, st);
+}
+
 extern "C" {
+
+int mc_fso_encode_raw(const void *src, void *dst, size_t n, int dtype, int t1, int t2, int astype,
+                      const void *offset, const void *scale, mc_stream_t stream) {
+  if (!x_valid(t1) || !x_valid(t2) || !offset || !scale) return MC_EINVAL;
+  if (x_is_time(t1) || x_is_time(t2)) return MC_EINVAL;  // numpy has no rint loop for them
+  return mc_ext_map(X_FSO_ENC, src, dst, n, dtype, t1, t2, astype, x_from_raw(offset, t1), x_from_raw(scale, t2), 1,
+                    1, (hipStream_t)stream);
+}
+
+int mc_fso_decode_raw(const void *src, void *dst, size_t n, int astype, int t3, int t4, int dtype,
+                      const void *scale, const void *offset, mc_stream_t stream) {
+  if (!x_valid(t3) || !x_valid(t4) || !offset || !scale) return MC_EINVAL;
+  auto floaty = [](int t) { return mc_is_float(t) || x_is_complex(t) || x_is_ld(t); };
+  if (!floaty(t3) || !floaty(t4)) return MC_EINVAL;
+  return mc_ext_map(X_FSO_DEC, src, dst, n, astype, t3, t4, dtype, x_from_raw(scale, t3), x_from_raw(offset, t4), 1,
+                    1, (hipStream_t)stream);
+}
+
+int mc_cast_calendar(const void *src, void *dst, size_t n, int from_dtype, int to_dtype, int src_unit,
+                     int64_t src_num, int dst_unit, int64_t dst_num, mc_stream_t stream) {
+  if (mc_dt_base(from_dtype) != MC_DT8 || mc_dt_base(to_dtype) != MC_DT8 || !x_valid(from_dtype) ||
+      !x_valid(to_dtype))
+    return MC_EINVAL;
+  if (src_unit < MC_DU_Y || src_unit > MC_DU_as || dst_unit < MC_DU_Y || dst_unit > MC_DU_as || src_num < 1 ||
+      dst_num < 1)
+    return MC_EINVAL;
+  const McX z = x_make(mc_num_i(0));
+  return mc_ext_map(X_CAL, src, dst, n, from_dtype, MC_DT8, MC_DT8, to_dtype, z, z, 1, 1, (hipStream_t)stream,
+                    src_unit, src_num, dst_unit, dst_num);
+}
 
 int mc_cast_units(const void *src, void *dst, size_t n, int from_dtype, int to_dtype, int64_t num, int64_t den,
                   mc_stream_t stream) {
@@ -703,7 +1068,7 @@ int mc_cast_units(const void *src, void *dst, size_t n, int from_dtype, int to_d
   if (same && num == 1 && den == 1) {
     if (n == 0) return MC_OK;
     if (!src || !dst) return MC_EINVAL;
-    const int es = x_is_complex(fb) ? mc_itemsize(x_comp(fb)) : x_itemsize(fb);
+    const int es = x_is_complex(fb) ? x_itemsize(x_comp(fb)) : x_itemsize(fb);
     const size_t ne = x_is_complex(fb) ? 2 * n : n;
     if (mc_dt_swapped(from_dtype) == mc_dt_swapped(to_dtype) || es == 1)
       return mc_copy_rows_impl(src, ne * es, dst, ne * es, ne * es, 1, st);

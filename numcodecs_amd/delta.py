@@ -68,22 +68,45 @@ def _dry_run_decode(astype, dtype):
     np.cumsum(np.zeros(2, dtype=astype), out=np.empty(2, dtype=dtype))
 
 
+_NUMERIC_KINDS = "biufcmM"
+
+
+def check_numeric(dtype, astype, encode) -> None:
+    """A string / bytes / void `dtype` or `astype`: the reference fails inside
+    numpy (delta.py:66 np.diff -> UFuncTypeError for the subtract loop;
+    delta.py:80 np.cumsum -> numpy's TypeError for add.accumulate), and so
+    does this codec, by running the same numpy call on a stand-in."""
+    d, a = np.dtype(dtype), np.dtype(astype)
+    if d.kind in _NUMERIC_KINDS and a.kind in _NUMERIC_KINDS:
+        return
+    if encode:
+        _dry_run_encode(d, a)
+    else:
+        _dry_run_decode(a, d)
+    raise NotImplementedError(f"Delta({d.str!r}, astype={a.str!r}) is not supported by the numcodecs_amd device "
+                              "kernels")
+
+
 def ext_delta_encode(src, dst, n, dtype, astype) -> None:
-    """Delta encode with a complex / timedelta64 / datetime64 side: the
-    differences in dtype (mc_ext.hip), cast to astype; a timedelta astype of
-    another unit through numpy's unit cast (mc_cast_units)."""
+    """Delta encode with a complex / timedelta64 / datetime64 / longdouble
+    side: the differences in dtype (mc_ext.hip), cast to astype.  A
+    timedelta64 / datetime64 pair with a unit change casts the first element
+    as numpy's scalar assignment does (delta.py:63: dtype -> astype, numpy's
+    astype rules -- a linear unit factor, the calendar path for years /
+    months, ticks kept between timedelta and datetime) and the differences
+    from timedelta64 in dtype's unit (delta.py:66)."""
     _dry_run_encode(dtype, astype)
     d, a = np.dtype(dtype), np.dtype(astype)
     if d.kind in "mM" and a.kind in "mM" and np.datetime_data(a) != np.datetime_data(d):
-        if d.kind == "M" or a.kind == "M":
-            # numpy converts the first element (a datetime scalar) and the
-            # differences (timedeltas) with different cast rules here
-            raise NotImplementedError(
-                f"Delta({d.str!r}, astype={a.str!r}): datetime64 with a unit change is not supported by the "
-                "numcodecs_amd device kernels")
+        unit, num = np.datetime_data(d)
+        diff_dt = np.dtype("m8" if unit == "generic" else f"m8[{num}{unit}]")
+        if d.byteorder == ">":
+            diff_dt = diff_dt.newbyteorder(">")
         tmp = torch.empty(n * 8, dtype=torch.uint8, device=src.device)
-        _ops.delta_encode(src, tmp, n, d, d)  # timedelta differences in dtype's unit
-        _ops.cast(tmp, dst, n, d, a)
+        _ops.delta_encode(src, tmp, n, d, diff_dt)  # timedelta differences in dtype's unit
+        if n > 1:
+            _ops.cast(tmp[8:], dst[a.itemsize:], n - 1, diff_dt, a)
+        _ops.cast(src, dst, 1, d, a)  # enc[0] = arr[0]
         return
     _ops.delta_encode(src, dst, n, d, a)
 
@@ -148,6 +171,7 @@ class Delta(Codec):
         if n == 0:  # enc[0] = arr[0] on an empty array (delta.py:63)
             raise IndexError("index 0 is out of bounds for axis 0 with size 0")
         check_first_elements(src.data[: self.dtype.itemsize], self.dtype, self.astype)
+        check_numeric(self.dtype, self.astype, True)
         dst = empty_like_bytes(n * self.astype.itemsize, src)
         if _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype):
             ext_delta_encode(src.data, dst, n, self.dtype, self.astype)
@@ -160,6 +184,7 @@ class Delta(Codec):
         if src.nbytes % self.astype.itemsize:
             raise ValueError("When changing to a larger dtype, its size must be a divisor of the total size")
         n = src.nbytes // self.astype.itemsize
+        check_numeric(self.dtype, self.astype, False)
         ext = _ops.is_ext_dtype(self.dtype) or _ops.is_ext_dtype(self.astype)
         loop = None if ext else decode_loop_dtype(self.astype, self.dtype)
         direct = device_out_bytes(out, n * self.dtype.itemsize, src)

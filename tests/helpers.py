@@ -119,3 +119,29 @@ def check_lab_build():
     if os.path.exists(marker):
         with open(marker) as f:
             pytest.fail(f"the lab library failed to build: {f.read().strip()}")
+
+
+def value_mask(dtype, nbytes: int) -> np.ndarray:
+    """Boolean byte mask of the bytes numpy defines for `nbytes` of `dtype`:
+    every byte, except the 6 padding bytes of each longdouble (component),
+    which numpy leaves as whatever its output buffer held ('<f16' bytes
+    10-15, '>f16' bytes 0-5; '<c32' / '>c32' per 16-byte component)."""
+    dt = np.dtype(dtype)
+    mask = np.ones(nbytes, dtype=bool)
+    if (dt.kind == "f" and dt.itemsize == 16) or (dt.kind == "c" and dt.itemsize == 32):
+        m = mask.reshape(-1, 16)
+        if dt.byteorder == ">":
+            m[:, :6] = False
+        else:
+            m[:, 10:] = False
+    return mask
+
+
+def same_values(got: bytes, want: bytes, dtype) -> bool:
+    """got == want on the bytes numpy defines for `dtype` (value_mask)."""
+    if len(got) != len(want):
+        return False
+    g = np.frombuffer(got, dtype=np.uint8)
+    w = np.frombuffer(want, dtype=np.uint8)
+    m = value_mask(dtype, len(g))
+    return bool(np.array_equal(g[m], w[m]))

@@ -60,7 +60,7 @@ def test_conversion_factor_reproduces_numpy(kind):
         for a in UNITS:
             for b in UNITS:
                 if kind == "M8" and (a in "YM") != (b in "YM"):
-                    continue  # calendar conversions: refused (NotImplementedError)
+                    continue  # calendar conversions: mc_cast_calendar (tests/test_x80.py)
                 src, dst = np.dtype(f"{kind}[{a}]"), np.dtype(f"{kind}[{b}]")
                 try:
                     want = t.view(src).astype(dst).view(np.int64)
@@ -95,8 +95,15 @@ def test_generic_units():
     with pytest.raises(ValueError):
         _ops.datetime_conversion_factor("m8[s]", "m8")
     assert _ops.time_cast_factor("m8[s]", "M8[ms]") == (1, 1)  # cross-kind: ticks kept
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):  # the calendar path is mc_cast_calendar's
         _ops.time_cast_factor("M8[Y]", "M8[D]")
+    assert _ops.calendar_cast("M8[Y]", "M8[3D]") == (0, 1, 3, 3)
+    assert _ops.calendar_cast("M8[2h]", "M8[M]") == (4, 2, 1, 1)
+    assert _ops.calendar_cast("M8[Y]", "M8[M]") is None  # linear (x12)
+    assert _ops.calendar_cast("m8[Y]", "m8[D]") is None  # timedelta: linear
+    assert _ops.calendar_cast("M8", "M8[Y]") is None  # generic
+    with pytest.raises(OverflowError):  # numpy's factor check comes first
+        _ops.calendar_cast("M8[Y]", "M8[as]")
 
 
 def test_dtype_codes():
@@ -109,7 +116,10 @@ def test_dtype_codes():
     with pytest.raises(NotImplementedError):
         _ops.dtype_code("S3")
     with pytest.raises(NotImplementedError):
-        _ops.dtype_code("<c32" if hasattr(np, "complex256") else "V8")
+        _ops.dtype_code("V8")
+    if np.finfo(np.longdouble).nmant == 63:  # x87 longdouble (round 6)
+        assert _ops.dtype_code("<f16") == _native.MC_F16L
+        assert _ops.dtype_code(">c32") == _native.MC_C32 | _native.MC_BIG_ENDIAN
 
 
 def test_header_codes_match():

@@ -160,12 +160,15 @@ def test_complex_warning_like_reference(device):
     assert out.cpu().tolist() == [1.0, 3.0]
 
 
-def test_datetime_calendar_cast_not_implemented(device):
-    """datetime64 calendar conversions (years/months <-> days) are refused
-    loudly, never computed wrong."""
-    x = np.arange(5, dtype="i8").view("M8[Y]")
-    with pytest.raises(NotImplementedError):
-        AsType(encode_dtype="M8[D]", decode_dtype="M8[Y]").encode(x)
+def test_datetime_calendar_cast_like_numpy(device):
+    """datetime64 calendar conversions (years/months <-> days; round 6:
+    csrc/mc_cal.h) give numpy's dates (the reference's astype.py:53 is
+    numpy's astype), both ways."""
+    x = np.array([0, 1, -1, 30, -2000, np.iinfo(np.int64).min, 7], dtype="i8").view("M8[Y]")
+    c = AsType(encode_dtype="M8[D]", decode_dtype="M8[Y]")
+    enc = c.encode(x)
+    assert enc.dtype == np.dtype("M8[D]") and enc.tobytes() == x.astype("M8[D]").tobytes()
+    assert c.decode(enc).tobytes() == x.tobytes()
 
 
 @pytest.mark.parametrize("dt", ["<c8", "<c16"])
