@@ -359,6 +359,20 @@ MC_DEV uint64_t fs_wave_min_fail(uint64_t first) {
   return first;
 }
 
+// A tile's prefix (the double every candidate of the tile is offset by).
+// Two-launch decode (with an arrival ticket): the group's exclusive prefix of
+// the tile's group (gpre, <= 64 groups of 2^gshift tiles) plus the tile's
+// exclusive prefix inside its group (ipre), both written by the reduce pass's
+// last arrivers; one add, so every reader (apply pass, walker) rebuilds
+// bitwise the same value.  Without a ticket (HIP-graph capture): ipre is the
+// whole prefix (k_fspec_pre) and gpre is null.
+struct FsPre {
+  const double *ipre;
+  const double *gpre;
+  unsigned gshift;
+  MC_DEV double at(size_t t) const { return gpre ? gpre[t >> gshift] + ipre[t] : ipre[t]; }
+};
+
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n, int a,
                                                           double *__restrict__ sums) {
@@ -373,11 +387,105 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__rest
   if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = (double)p[FS_Q - 1][W - 1];
 }
 
+// Two-launch form (k_fspec_pre's launch folded in): as
+// k_fspec_reduce, and the tile also resets its failure word (and tile 0 the
+// first-failure word) for the apply pass.  Each tile then arrives on its
+// group's ticket word; the group's last arriver computes the group's
+// exclusive in-group prefixes (ipre) and total, and the last group to finish
+// scans the <= 64 group totals into gpre (fixed association throughout;
+// any association works, the apply pass only proposes candidates from them).
+// Ticket words are left zero.  Hand-offs: every total is stored, then an
+// agent-scope release and the arrival; the last arriver's acquire precedes
+// the workgroup barrier and the loads (MI355X_MICROARCH.md, correctness
+// boundaries).
+template <int A_, int D, int SW = 0>
+__global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__restrict__ src, size_t n, int a,
+                                                            double *__restrict__ sums, double *__restrict__ ipre,
+                                                            double *__restrict__ gtot, double *__restrict__ gpre,
+                                                            uint64_t *__restrict__ tfail, uint64_t *__restrict__ fail,
+                                                            uint32_t *__restrict__ ticket, size_t ntiles,
+                                                            unsigned gshift) {
+  using Tr = FsT<A_, D>;
+  using P = typename Tr::P;
+  constexpr int W = Tr::W;
+  __shared__ P lds[FS_Q][MC_BLOCK / 64];
+  __shared__ double wsum[MC_BLOCK / 64];
+  __shared__ int role;  // 0: done, 1: last of its group, 2: also the last group
+  const size_t tile = blockIdx.x;
+  {
+    typename Tr::V v[FS_Q][W];
+    fs_load<A_, D, SW>(src, n, tile * fs_tile<D>(), a, v);
+    P p[FS_Q][W];
+    fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
+    if (threadIdx.x == MC_BLOCK - 1) {
+      sums[tile] = (double)p[FS_Q - 1][W - 1];
+      tfail[tile] = ~(uint64_t)0;
+      if (tile == 0) *fail = n;
+      __threadfence();  // release the total before arriving
+      const size_t g = tile >> gshift;
+      const size_t left = ntiles - (g << gshift);
+      const unsigned in_group = (unsigned)(left < ((size_t)1 << gshift) ? left : ((size_t)1 << gshift));
+      const bool last = atomicAdd(&ticket[MC_ARRIVAL_LINE * g], 1u) == in_group - 1u;
+      if (last) __threadfence();  // acquire: the group's totals
+      role = last ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (role == 0) return;
+  // the group's exclusive prefixes: thread t owns K = 2^gshift / MC_BLOCK
+  // consecutive tiles (sequential), then a block scan of the thread totals
+  const size_t g = tile >> gshift, g0 = g << gshift;
+  const size_t cnt = (ntiles - g0) < ((size_t)1 << gshift) ? (ntiles - g0) : ((size_t)1 << gshift);
+  const unsigned K = (1u << gshift) / MC_BLOCK;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double own[8];  // K <= 8 (at most 2048 tiles per group)
+  double tsum = 0.0;
+#pragma unroll
+  for (unsigned k = 0; k < 8; ++k) {
+    const size_t j = (size_t)threadIdx.x * K + k;
+    own[k] = (k < K && j < cnt) ? sums[g0 + j] : 0.0;
+  }
+#pragma unroll
+  for (unsigned k = 0; k < 8; ++k) tsum += own[k];
+  const double incl = mc_wave_scan_f64(tsum);
+  const double ex = mc_wave_shr1_f64(incl);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  double base = 0.0, tot = 0.0;
+#pragma unroll
+  for (int w = 0; w < MC_BLOCK / 64; ++w) {
+    if (w < wave) base += wsum[w];
+    tot += wsum[w];
+  }
+  double run = base + (lane ? ex : 0.0);
+#pragma unroll
+  for (unsigned k = 0; k < 8; ++k) {
+    const size_t j = (size_t)threadIdx.x * K + k;
+    if (k < K && j < cnt) ipre[g0 + j] = run;
+    run += own[k];
+  }
+  if (threadIdx.x == 0) {
+    gtot[g] = tot;
+    ticket[MC_ARRIVAL_LINE * g] = 0;  // every arrival of the group is in
+    __threadfence();
+    const unsigned ngroups = (unsigned)((ntiles + ((size_t)1 << gshift) - 1) >> gshift);
+    const bool last = atomicAdd(&ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS], 1u) == ngroups - 1u;
+    if (last) {
+      __threadfence();
+      double acc = 0.0;
+      for (unsigned k = 0; k < ngroups; ++k) {
+        gpre[k] = acc;
+        acc += gtot[k];
+      }
+      ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS] = 0;
+    }
+  }
+}
+
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restrict__ src,
                                                          uint8_t *__restrict__ dst, size_t n, int a,
-                                                         const double *__restrict__ sums,
-                                                         const double *__restrict__ pre_t,
+                                                         const double *__restrict__ sums, FsPre pre_t,
                                                          uint64_t *__restrict__ tfail,
                                                          uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
@@ -396,7 +504,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   fs_load<A_, D, SW>(src, n, t0, a, v);
   P p[FS_Q][W];
   fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
-  const P Sp = (P)pre_t[tile];  // the tile's prefix
+  const P Sp = (P)pre_t.at(tile);  // the tile's prefix
   S c[FS_Q][W], up[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -408,7 +516,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   __syncthreads();
   // the tile's last candidate in the previous tile: the same double sum it
   // was rounded from there (sums[] is that tile's last prefix, bitwise)
-  const S pbound = tile ? Tr::bound(pre_t[tile - 1], sums[tile - 1]) : (S)0;
+  const S pbound = tile ? Tr::bound(pre_t.at(tile - 1), sums[tile - 1]) : (S)0;
   S p0[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -903,8 +1011,7 @@ template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restrict__ src, size_t src_stride,
                                                         uint8_t *__restrict__ dst, size_t dst_stride, size_t n,
                                                         int a, uint64_t *__restrict__ rowfail,
-                                                        const double *__restrict__ sums,
-                                                        const double *__restrict__ pre,
+                                                        const double *__restrict__ sums, FsPre pre,
                                                         const uint64_t *__restrict__ tfail,
                                                         const uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
@@ -942,7 +1049,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     if (f >= n) return;        // everything verified: dst is final
     t = (size_t)(f / TE);
     has_in = t > 0;
-    if (has_in) yin = Tr::bound(pre[t - 1], sums[t - 1]);  // tile t-1 verified: its last candidate
+    if (has_in) yin = Tr::bound(pre.at(t - 1), sums[t - 1]);  // tile t-1 verified: its last candidate
   } else {
     // a row that k_fspec_rows left at its first failing tile (rowfail = its
     // start; n when the row verified): resume there from the last stored value
@@ -969,12 +1076,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
       t = te;
       if (t >= ntiles) break;
       fsw_load<A_, D, SW>(src, n, t * (size_t)TE, a, nv);
-      if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t - 1], sums[t - 1]))) {
+      if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre.at(t - 1), sums[t - 1]))) {
         const size_t nt = fsw_next_failed(tfail, t, ntiles, ldsx);
         if (nt >= ntiles) break;
         if (nt != t) {
           t = nt;
-          yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
+          yin = Tr::bound(pre.at(nt - 1), sums[nt - 1]);
           fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         }
         serial_run = 0;
@@ -1161,13 +1268,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     has_in = true;
     fsw_store<A_, D, SW>(dst, n, t0, c);
     if (t + 1 >= ntiles) break;
-    if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t], sums[t]))) {
+    if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre.at(t), sums[t]))) {
       // in sync with the apply pass: tiles that verified there are final
       const size_t nt = fsw_next_failed(tfail, t + 1, ntiles, ldsx);
       if (nt >= ntiles) break;
       if (nt != t + 1) {
         t = nt;
-        yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
+        yin = Tr::bound(pre.at(nt - 1), sums[nt - 1]);
         fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         continue;
       }
@@ -1243,16 +1350,31 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict
   if (blockIdx.x == 0 && threadIdx.x == 0) *fail = n;
 }
 
+// Workspace (fspec_ws_bytes): sums, pre / ipre, tfail (ntiles words each),
+// 64 group totals, 64 group prefixes, then fail (the last word).  With an arrival ticket
+// the tile prefixes come out of the reduce pass (k_fspec_reduce_g: three
+// launches); without one (HIP-graph capture) k_fspec_pre computes them.
 template <int A_, int D, int SW = 0>
-static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st) {
+static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, uint32_t *ticket, hipStream_t st) {
   const size_t ntiles = fspec_ntiles(n, D);
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
-  uint64_t *tfail = reinterpret_cast<uint64_t *>(pre + ntiles), *fail = tfail + ntiles;
-  k_fspec_reduce<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
-  k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail, n);
-  k_fspec_apply<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, pre, tfail, fail);
+  uint64_t *tfail = reinterpret_cast<uint64_t *>(pre + ntiles), *fail = tfail + ntiles + 2 * FS_MAX_GROUPS;
+  double *gtot = reinterpret_cast<double *>(tfail + ntiles), *gpre = gtot + FS_MAX_GROUPS;
+  FsPre fp{pre, nullptr, 0};
+  if (ticket) {
+    unsigned gshift = 8;  // >= MC_BLOCK tiles per group, at most FS_MAX_GROUPS groups
+    while ((ntiles + ((size_t)1 << gshift) - 1) >> gshift > FS_MAX_GROUPS) ++gshift;
+    fp = FsPre{pre, gpre, gshift};
+    k_fspec_reduce_g<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums, pre, gtot, gpre, tfail, fail,
+                                                                       ticket, ntiles, gshift);
+  } else {
+    k_fspec_reduce<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
+    k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail,
+                                                                                     n);
+  }
+  k_fspec_apply<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, fp, tfail, fail);
   // one walker from the first failing tile (returns at once if none failed)
-  k_fspec_walk<A_, D, SW><<<1, MC_BLOCK, 0, st>>>(s, 0, d, 0, n, a, nullptr, sums, pre, tfail, fail);
+  k_fspec_walk<A_, D, SW><<<1, MC_BLOCK, 0, st>>>(s, 0, d, 0, n, a, nullptr, sums, fp, tfail, fail);
 }
 
 // the speculative rows pass, then one walker per row that failed (rows that
@@ -1261,8 +1383,8 @@ template <int A_, int D, int SW = 0>
 static void launch_fspec_rows(const uint8_t *sc, size_t src_stride, uint8_t *dc, size_t dst_stride, size_t n, int a,
                               uint64_t *fail, unsigned g, hipStream_t st) {
   k_fspec_rows<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
-  k_fspec_walk<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr, nullptr,
-                                                nullptr, nullptr);
+  k_fspec_walk<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr,
+                                                FsPre{nullptr, nullptr, 0}, nullptr, nullptr);
 }
 
 }  // namespace

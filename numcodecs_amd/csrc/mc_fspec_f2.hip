@@ -3,9 +3,9 @@
 // (mc_fspec_f2_be.hip) so that the instances build in parallel.
 #include "mc_fspec.h"
 
-void mc_fspec_launch_f2(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st) {
-  if (a == MC_F2) return launch_fspec<MC_F2, MC_F2>(s, d, n, a, ws, st);
-  launch_fspec<-1, MC_F2>(s, d, n, a, ws, st);
+void mc_fspec_launch_f2(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, uint32_t *ticket, hipStream_t st) {
+  if (a == MC_F2) return launch_fspec<MC_F2, MC_F2>(s, d, n, a, ws, ticket, st);
+  launch_fspec<-1, MC_F2>(s, d, n, a, ws, ticket, st);
 }
 
 void mc_fspec_rows_launch_f2(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,

@@ -3,9 +3,9 @@
 // (mc_fspec_f4_be.hip) so that the instances build in parallel.
 #include "mc_fspec.h"
 
-void mc_fspec_launch_f4(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st) {
-  if (a == MC_F4) return launch_fspec<MC_F4, MC_F4>(s, d, n, a, ws, st);
-  launch_fspec<-1, MC_F4>(s, d, n, a, ws, st);
+void mc_fspec_launch_f4(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, uint32_t *ticket, hipStream_t st) {
+  if (a == MC_F4) return launch_fspec<MC_F4, MC_F4>(s, d, n, a, ws, ticket, st);
+  launch_fspec<-1, MC_F4>(s, d, n, a, ws, ticket, st);
 }
 
 void mc_fspec_rows_launch_f4(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,

@@ -6,10 +6,10 @@
 // big-endian output.
 #include "mc_fspec.h"
 
-void mc_fspec_launch_be_f8(const uint8_t *s, uint8_t *d, size_t n, int a, bool swo, void *ws, hipStream_t st) {
-  if (swo && a == (MC_F8 | MC_BIG_ENDIAN)) launch_fspec<MC_F8, MC_F8, 3>(s, d, n, a, ws, st);
-  else if (swo) launch_fspec<-1, MC_F8, 2>(s, d, n, a, ws, st);
-  else mc_fspec_launch_f8(s, d, n, a, ws, st);  // flagged a != MC_F8: the runtime-astype instance
+void mc_fspec_launch_be_f8(const uint8_t *s, uint8_t *d, size_t n, int a, bool swo, void *ws, uint32_t *ticket, hipStream_t st) {
+  if (swo && a == (MC_F8 | MC_BIG_ENDIAN)) launch_fspec<MC_F8, MC_F8, 3>(s, d, n, a, ws, ticket, st);
+  else if (swo) launch_fspec<-1, MC_F8, 2>(s, d, n, a, ws, ticket, st);
+  else mc_fspec_launch_f8(s, d, n, a, ws, ticket, st);  // flagged a != MC_F8: the runtime-astype instance
 }
 
 void mc_fspec_rows_launch_be_f8(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a, bool swo,

@@ -477,19 +477,24 @@ static inline bool fspec_types_ok(int astype, int dtype) {
          mc_float_loop_dtype(astype, dtype) == mc_dt_base(dtype);
 }
 
-// tile totals, tile prefixes, per-tile first failures, the first failure
-// (the last word, read by the tests)
-static inline size_t fspec_ws_bytes(size_t n, int dt) { return (3 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
+// tile totals, tile prefixes, per-tile first failures, group totals, group
+// prefixes, the first failure (the last word, read by the tests)
+constexpr size_t FS_MAX_GROUPS = 64;
+static inline size_t fspec_ws_bytes(size_t n, int dt) {
+  return (3 * fspec_ntiles(n, dt) + 1 + 2 * FS_MAX_GROUPS) * sizeof(uint64_t);
+}
 
 // speculative float Delta decode of one chunk (workspace fspec_ws_bytes) /
 // of `g` rows (fail: one word per row), output dtype f2 / f4 / f8, any
 // astype whose loop dtype is the output dtype (mc_fspec_f*.hip); the _be_
 // twins take a big-endian astype `a` and/or output (swo)
 #define MC_FSPEC_DECL(T)                                                                                          \
-  void mc_fspec_launch_##T(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, hipStream_t st);            \
+  void mc_fspec_launch_##T(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, uint32_t *ticket,          \
+                           hipStream_t st);                                                                    \
   void mc_fspec_rows_launch_##T(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,           \
                                 uint64_t *fail, unsigned g, hipStream_t st);                                   \
-  void mc_fspec_launch_be_##T(const uint8_t *s, uint8_t *d, size_t n, int a, bool swo, void *ws, hipStream_t st); \
+  void mc_fspec_launch_be_##T(const uint8_t *s, uint8_t *d, size_t n, int a, bool swo, void *ws,                 \
+                              uint32_t *ticket, hipStream_t st);                                               \
   void mc_fspec_rows_launch_be_##T(const uint8_t *sc, size_t ss, uint8_t *dc, size_t ds, size_t n, int a,        \
                                    bool swo, uint64_t *fail, unsigned g, hipStream_t st);
 MC_FSPEC_DECL(f2)

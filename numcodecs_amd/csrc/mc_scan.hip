@@ -726,19 +726,20 @@ static void launch_dscan(const uint8_t *s, uint8_t *d, size_t n, uint64_t *ws, h
 // build time)
 static bool fspec_enabled() { return mc_sched.fspec != 0; }
 
-static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int dt, void *ws, hipStream_t st) {
+static void launch_fspec_any(const uint8_t *s, uint8_t *d, size_t n, int a, int dt, void *ws, uint32_t *ticket,
+                             hipStream_t st) {
   const bool swo = mc_dt_swapped(dt);
   dt = mc_dt_base(dt);
   if (swo || mc_dt_swapped(a)) {
-    if (dt == MC_F8) mc_fspec_launch_be_f8(s, d, n, a, swo, ws, st);
-    else if (dt == MC_F4) mc_fspec_launch_be_f4(s, d, n, a, swo, ws, st);
-    else mc_fspec_launch_be_f2(s, d, n, a, swo, ws, st);
+    if (dt == MC_F8) mc_fspec_launch_be_f8(s, d, n, a, swo, ws, ticket, st);
+    else if (dt == MC_F4) mc_fspec_launch_be_f4(s, d, n, a, swo, ws, ticket, st);
+    else mc_fspec_launch_be_f2(s, d, n, a, swo, ws, ticket, st);
   } else if (dt == MC_F8) {
-    mc_fspec_launch_f8(s, d, n, a, ws, st);
+    mc_fspec_launch_f8(s, d, n, a, ws, ticket, st);
   } else if (dt == MC_F4) {
-    mc_fspec_launch_f4(s, d, n, a, ws, st);
+    mc_fspec_launch_f4(s, d, n, a, ws, ticket, st);
   } else {
-    mc_fspec_launch_f2(s, d, n, a, ws, st);
+    mc_fspec_launch_f2(s, d, n, a, ws, ticket, st);
   }
 }
 
@@ -832,7 +833,7 @@ int mc_delta_decode(const void *src, void *dst, size_t n, int astype, int dtype,
     if (fspec_types_ok(astype, dtype) && fspec_enabled() && workspace &&
         workspace_bytes >= fspec_ws_bytes(n, dtype) && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
         (uintptr_t)workspace % 8 == 0) {
-      launch_fspec_any(s, d, n, astype, dtype, workspace, st);
+      launch_fspec_any(s, d, n, astype, dtype, workspace, ticket, st);
       fix_first_elems(s, 0, d, 0, 1, astype, dtype, st);
       return mc_last_launch();
     }

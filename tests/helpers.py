@@ -145,3 +145,32 @@ def same_values(got: bytes, want: bytes, dtype) -> bool:
     w = np.frombuffer(want, dtype=np.uint8)
     m = value_mask(dtype, len(g))
     return bool(np.array_equal(g[m], w[m]))
+
+
+def delta_decode_both_schedules(src, dst, n, a, d, ws_n):
+    """mc_delta_decode of device bytes `src` into `dst` twice: with a fresh
+    arrival ticket (the product's schedule: the float decode's tile prefixes
+    folded into its reduce pass) and without one (the HIP-graph-capture
+    schedule, k_fspec_pre).  Both must give the same bytes and the same
+    first-failure word (the workspace's last word, returned; None without a
+    workspace); the ticket must be left zero."""
+    import torch
+
+    from numcodecs_amd import _native, _ops
+
+    out, words = [], []
+    for with_ticket in (True, False):
+        ws = torch.zeros(max(ws_n // 8, 1), dtype=torch.int64, device=src.device)
+        ticket = torch.zeros(_native.MC_ARRIVAL_WORDS, dtype=torch.int32, device=src.device)
+        dst.fill_(0xA5 if dst.dtype == torch.uint8 else 0)
+        _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d,
+                                                  ws.data_ptr() if ws_n else None, ws_n,
+                                                  ticket.data_ptr() if with_ticket else None, _ops.stream(src)),
+                      "mc_delta_decode")
+        torch.cuda.synchronize()
+        assert int(ticket.abs().sum()) == 0, "arrival ticket not left zero"
+        out.append(dst.cpu().numpy().tobytes())
+        words.append(int(ws[-1].item()) if ws_n else None)
+    assert out[0] == out[1], "ticket / ticket-free schedules differ"
+    assert words[0] == words[1], words
+    return words[0]

@@ -14,6 +14,7 @@ import torch
 
 import oracle
 from numcodecs_amd import Delta, _native, _ops
+from tests.helpers import delta_decode_both_schedules
 
 pytestmark = pytest.mark.gpu
 
@@ -58,12 +59,10 @@ def _decode_raw(enc_np, dt):
     a = _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    assert ws_n == (3 * ntiles + 1) * 8  # totals, prefixes, per-tile failures, first failure
-    ws = torch.zeros(ws_n // 8, dtype=torch.int64, device=dev)
-    _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
-                                              None, _ops.stream(src)), "mc_delta_decode")
-    torch.cuda.synchronize()
-    return dst.cpu().numpy(), int(ws[-1].item())
+    # totals, prefixes, per-tile failures, 64 group totals / prefixes, first failure
+    assert ws_n == (3 * ntiles + 1 + 128) * 8
+    first = delta_decode_both_schedules(src, dst, n, a, a, ws_n)
+    return dst.cpu().numpy(), first
 
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])
@@ -155,10 +154,9 @@ def test_repeated_calls_reset_failure_word(device, dt):
     for enc in (bad, good, bad, good):
         src = torch.from_numpy(enc).to(dev)
         dst = torch.empty_like(src)
-        _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, a, ws.data_ptr(), ws_n,
-                                                  None, _ops.stream(src)), "mc_delta_decode")
+        first = delta_decode_both_schedules(src, dst, n, a, a, ws_n)
         assert dst.cpu().numpy().tobytes() == _oracle_dec(enc, dt).tobytes()
-        assert int(ws[-1].item()) == (n if enc is good else 7)
+        assert first == (n if enc is good else 7)
 
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])

@@ -17,6 +17,7 @@ import torch
 
 import oracle
 from numcodecs_amd import Delta, _native, _ops, batch
+from tests.helpers import delta_decode_both_schedules
 
 pytestmark = pytest.mark.gpu
 
@@ -50,13 +51,9 @@ def _decode_raw(enc_np, dt, at):
     a, d = _ops.dtype_code(at), _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, d)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    assert ws_n == ((3 * ntiles + 1) * 8 if _speculative(dt, at) else 0)
-    ws = torch.zeros(max(ws_n // 8, 1), dtype=torch.int64, device=dev)
-    _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d,
-                                              ws.data_ptr() if ws_n else None, ws_n, None, _ops.stream(src)),
-                  "mc_delta_decode")
-    torch.cuda.synchronize()
-    return dst.cpu().numpy().view(np.dtype(dt)), (int(ws[-1].item()) if ws_n else None)
+    assert ws_n == ((3 * ntiles + 1 + 128) * 8 if _speculative(dt, at) else 0)
+    first = delta_decode_both_schedules(src, dst, n, a, d, ws_n)
+    return dst.cpu().numpy().view(np.dtype(dt)), first
 
 
 def _speculative(dt, at):

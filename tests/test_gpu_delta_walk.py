@@ -16,6 +16,7 @@ import torch
 
 import oracle
 from numcodecs_amd import Delta, _native, _ops, batch
+from tests.helpers import delta_decode_both_schedules
 
 pytestmark = pytest.mark.gpu
 
@@ -71,11 +72,8 @@ def _decode_raw(enc_np, dt, at=None):
     dst = torch.empty(n * np.dtype(dt).itemsize, dtype=torch.uint8, device=dev)
     a, d = _ops.dtype_code(at), _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, d)
-    ws = torch.zeros(max(ws_n // 8, 1), dtype=torch.int64, device=dev)
-    _native.check(_native.lib.mc_delta_decode(src.data_ptr(), dst.data_ptr(), n, a, d, ws.data_ptr(), ws_n,
-                                              None, _ops.stream(src)), "mc_delta_decode")
-    torch.cuda.synchronize()
-    return dst.cpu().numpy().view(np.dtype(dt)), int(ws[-1].item())
+    first = delta_decode_both_schedules(src, dst, n, a, d, ws_n)
+    return dst.cpu().numpy().view(np.dtype(dt)), first
 
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8", "<f2"])
