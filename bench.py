@@ -44,6 +44,7 @@ Printed (rank 0): ONE JSON line with the contract's keys plus
 from __future__ import annotations
 
 import argparse
+import csv
 import glob
 import json
 import os
@@ -340,6 +341,36 @@ def pmc_traffic():
     if not vals:
         return None, None
     return int(sum(vals) / len(vals)), os.path.relpath(files[-1], ROOT)
+
+
+# the headline kernels as rocprofv3 names them (dispatch defaults for one
+# 256 MiB chunk, numcodecs_amd/csrc/mc_shuffle.hip default_variant)
+HEADLINE_KERNELS = {"encode": "k_shuffle_enc<4, false, false, false, true, 8>", "decode": "k_shuffle4_dec_pair<true, 2>"}
+
+
+def trace_roofline():
+    """The headline kernels' rocprof averages from the newest
+    profiles/*/kernel_stats_headline.csv (the bench under rocprofv3 --stats,
+    committed with the round): algorithmic bytes per launch (2 x 256 MiB) /
+    average duration / peak, per kernel and for the dominant (slower) one --
+    the figure a reader can tie to profiles/, beside this run's event-timed
+    `frac` (a different box and run: the two agree within the box spread)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "kernel_stats_headline.csv")))
+    if not files:
+        return None
+    avg = {}
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            for role, name in HEADLINE_KERNELS.items():
+                if name in row["Name"]:
+                    avg[role] = float(row["AverageNs"]) * 1e-9
+    if len(avg) != 2:
+        return None
+    per = {role: {"kernel": HEADLINE_KERNELS[role], "avg_us": round(t * 1e6, 2),
+                  "frac": round(2 * CHUNK / t / 1e9 / PEAK_GBPS, 4)} for role, t in avg.items()}
+    dom = max(per, key=lambda r: avg[r])
+    return {"trace_frac": per[dom]["frac"], "trace_kernel": per[dom]["kernel"],
+            "trace_file": os.path.relpath(files[-1], ROOT), "trace_kernels": per}
 
 
 def run_step_timing(args, dev, dist, rank):
@@ -894,6 +925,7 @@ def main():
                 "copy_ceiling_GBps": ceiling["ceiling_GBps"],
                 "frac_of_copy_ceiling": round(achieved / ceiling["ceiling_GBps"], 4),
                 "copy_calibration": ceiling,
+                **(trace_roofline() or {"trace_frac": None}),
             },
             "c5_sharded": {
                 "GiBps": round(c5_bytes / GiB / c5_t, 1),

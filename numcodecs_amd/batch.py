@@ -22,7 +22,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _native, _ops
+from . import _native, _ops, multi
 from ._native import check, lib
 from .bitround import BitRound, max_bits
 from .compat import device_out_bytes, ensure_contiguous_ndarray, is_device_tensor
@@ -611,12 +611,20 @@ def host_pipeline(host_in: torch.Tensor, host_out: torch.Tensor, elementsize: in
     default slice is ~64 MiB: measured on MI355X (tools/probe_e2e.py) 64-128
     MiB slices reach 43-44 GiB/s host->host against 45 GiB/s of concurrent
     H2D+D2H, while 8-16 MiB slices drop to ~24 GiB/s.
+
+    ``devices=[...]`` splits the rows into contiguous ranges, one worker
+    thread and one such ring per entry (numcodecs_amd.multi.host_rows), so
+    several GPUs' PCIe links and kernels work on the batch at once.
     """
     _native.require_device()
     if host_in.device.type != "cpu" or host_out.device.type != "cpu":
         raise TypeError("host_pipeline takes CPU tensors (pinned for overlap)")
     if host_in.shape != host_out.shape or host_in.dim() != 2:
         raise ValueError("host_in and host_out must be [B, chunk_bytes] of equal shape")
+    if devices is not None:
+        multi.host_rows(lambda dev, lo, hi: host_pipeline(host_in[lo:hi], host_out[lo:hi], elementsize, encode,
+                                                          slice_chunks, nslots, dev), host_in.shape[0], devices)
+        return
     device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     b, n = host_in.shape
     if b == 0 or n == 0:

@@ -151,18 +151,25 @@ def _fused_c4_at(codecs, i):
     return i + 3 <= len(codecs) and batch._c4_scalars(*codecs[i:i + 3]) is not None
 
 
-def encode_chunks(codecs, chunks: torch.Tensor, devices=None) -> torch.Tensor:
+def encode_chunks(codecs, chunks, devices=None, allow_peer_copy=False):
     """Encode every row of the device batch `chunks` ([B, ...], typed as the
     first codec expects) through `codecs` in order; returns [B, m].  A
     FixedScaleOffset -> Delta -> Shuffle run encodes in one fused launch.
-    ``devices=[...]`` spreads contiguous row ranges over those GPUs, one
-    worker thread each (numcodecs_amd.multi); the result is gathered in row
-    order on `chunks`' device."""
-    if not is_device_tensor(chunks) or chunks.dim() < 1:
-        raise TypeError("encode_chunks takes a device tensor [B, ...]")
+
+    Multi-GPU (numcodecs_amd.multi): `chunks` may be a list of per-device
+    resident shards (one tensor per GPU); each is encoded on its own device
+    and the list of results is returned, each left on its device.
+    ``devices=[...]`` with one tensor splits its row ranges over workers of
+    that tensor's device; other GPUs are refused unless
+    ``allow_peer_copy=True`` (rows copied over xGMI and back)."""
     codecs = list(codecs)
+    if isinstance(chunks, (list, tuple)):
+        ys, _ = multi.device_shards(lambda d: (encode_chunks(codecs, d), None), chunks)
+        return ys
+    if not is_device_tensor(chunks) or chunks.dim() < 1:
+        raise TypeError("encode_chunks takes a device tensor [B, ...] or a list of them")
     if devices is not None:
-        y, _ = multi.device_rows(lambda d: (encode_chunks(codecs, d), None), chunks, devices)
+        y, _ = multi.device_rows(lambda d: (encode_chunks(codecs, d), None), chunks, devices, allow_peer_copy)
         return y
     x = chunks.reshape(chunks.shape[0], -1)
     i = 0
@@ -178,21 +185,26 @@ def encode_chunks(codecs, chunks: torch.Tensor, devices=None) -> torch.Tensor:
     return x
 
 
-def decode_chunks(codecs, chunks: torch.Tensor, _pending=None, devices=None) -> torch.Tensor:
+def decode_chunks(codecs, chunks, _pending=None, devices=None, allow_peer_copy=False):
     """Invert :func:`encode_chunks` (codecs given in encode order); raises
     the codec's RuntimeError if any row's checksum does not match.
-    ``devices=[...]``: as for encode_chunks; the checksum comparisons of all
-    workers are made after they finish, chain step by chain step and row
-    range by row range -- the mismatch the one-device call would raise."""
-    if not is_device_tensor(chunks) or chunks.dim() < 1:
-        raise TypeError("decode_chunks takes a device tensor [B, ...]")
+    Resident shards / ``devices=[...]``: as for encode_chunks; the checksum
+    comparisons of all workers are made after they finish, chain step by
+    chain step and row range by row range -- the mismatch the one-device
+    call would raise."""
     codecs = list(codecs)
-    if devices is not None:
+    shards = isinstance(chunks, (list, tuple))
+    if not shards and (not is_device_tensor(chunks) or chunks.dim() < 1):
+        raise TypeError("decode_chunks takes a device tensor [B, ...] or a list of them")
+    if shards or devices is not None:
         def one(d):
             pend = []
             return decode_chunks(codecs, d, pend), pend
 
-        y, pends = multi.device_rows(one, chunks, devices)
+        if shards:
+            y, pends = multi.device_shards(one, chunks)
+        else:
+            y, pends = multi.device_rows(one, chunks, devices, allow_peer_copy)
         steps = [[p[k] for p in pends] for k in range(len(pends[0]))] if pends and pends[0] else []
         for step in steps:
             for c, sums, stored in step:

@@ -366,6 +366,8 @@ MC_DEV uint64_t fs_wave_min_fail(uint64_t first) {
 // last arrivers; one add, so every reader (apply pass, walker) rebuilds
 // bitwise the same value.  Without a ticket (HIP-graph capture): ipre is the
 // whole prefix (k_fspec_pre) and gpre is null.
+constexpr int FS_RG = 4;  // tiles per k_fspec_reduce_g workgroup (divides every group)
+
 struct FsPre {
   const double *ipre;
   const double *gpre;
@@ -388,16 +390,19 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__rest
 }
 
 // Two-launch form (k_fspec_pre's launch folded in): as
-// k_fspec_reduce, and the tile also resets its failure word (and tile 0 the
-// first-failure word) for the apply pass.  Each tile then arrives on its
+// k_fspec_reduce over FS_RG consecutive tiles per workgroup (one arrival per
+// FS_RG tiles: with one tile each, the 16 Ki returning arrivals of 256 MiB
+// f4 kept every workgroup alive an atomic round trip longer, 58 against
+// 44 us), and each tile also resets its failure word (tile 0 the
+// first-failure word) for the apply pass.  The workgroup then arrives on its
 // group's ticket word; the group's last arriver computes the group's
 // exclusive in-group prefixes (ipre) and total, and the last group to finish
 // scans the <= 64 group totals into gpre (fixed association throughout;
 // any association works, the apply pass only proposes candidates from them).
-// Ticket words are left zero.  Hand-offs: every total is stored, then an
-// agent-scope release and the arrival; the last arriver's acquire precedes
-// the workgroup barrier and the loads (MI355X_MICROARCH.md, correctness
-// boundaries).
+// Ticket words are left zero.  Hand-offs inside the launch: every total is
+// an agent-scope (sc1) store drained by `s_waitcnt vmcnt(0)` before the
+// arrival, and the last arriver reads them with agent-scope loads
+// (MI355X_MICROARCH.md, correctness boundaries, the sc1 form).
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__restrict__ src, size_t n, int a,
                                                             double *__restrict__ sums, double *__restrict__ ipre,
@@ -408,26 +413,47 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__re
   using Tr = FsT<A_, D>;
   using P = typename Tr::P;
   constexpr int W = Tr::W;
-  __shared__ P lds[FS_Q][MC_BLOCK / 64];
+  __shared__ P lds[FS_RG][FS_Q][MC_BLOCK / 64];
   __shared__ double wsum[MC_BLOCK / 64];
-  __shared__ int role;  // 0: done, 1: last of its group, 2: also the last group
-  const size_t tile = blockIdx.x;
+  __shared__ int role;  // 1: the last arrival of its group
+  const size_t tile = (size_t)blockIdx.x * FS_RG;  // this workgroup's first tile
+  const int cnt_t = (int)(ntiles - tile < (size_t)FS_RG ? ntiles - tile : (size_t)FS_RG);
   {
-    typename Tr::V v[FS_Q][W];
-    fs_load<A_, D, SW>(src, n, tile * fs_tile<D>(), a, v);
-    P p[FS_Q][W];
-    fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
+    typename Tr::V v[FS_RG][FS_Q][W];
+    if ((tile + FS_RG) * fs_tile<D>() <= n) {
+      // FS_RG whole tiles: every load issued before the first scan
+#pragma unroll
+      for (int r = 0; r < FS_RG; ++r) fs_load<A_, D, SW>(src, n, (tile + r) * fs_tile<D>(), a, v[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < FS_RG; ++r)
+        if (r < cnt_t) fs_load<A_, D, SW>(src, n, (tile + r) * fs_tile<D>(), a, v[r]);
+    }
+    P tot[FS_RG];
+#pragma unroll
+    for (int r = 0; r < FS_RG; ++r) {
+      P p[FS_Q][W];
+      fs_tile_scan<typename Tr::V, W, P>(v[r], p, lds[r]);
+      tot[r] = p[FS_Q - 1][W - 1];
+    }
     if (threadIdx.x == MC_BLOCK - 1) {
-      sums[tile] = (double)p[FS_Q - 1][W - 1];
-      tfail[tile] = ~(uint64_t)0;
+      // the totals are handed to the group's last arriver inside this launch:
+      // agent-scope stores drained before the arrival (no release fence: an
+      // agent-scope fence writes back the XCD's L2 in every workgroup)
+#pragma unroll
+      for (int r = 0; r < FS_RG; ++r) {
+        if (r < cnt_t) {
+          __hip_atomic_store(reinterpret_cast<uint64_t *>(sums) + tile + r, __builtin_bit_cast(uint64_t, (double)tot[r]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tfail[tile + r] = ~(uint64_t)0;  // read by the next launch
+        }
+      }
       if (tile == 0) *fail = n;
-      __threadfence();  // release the total before arriving
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const size_t g = tile >> gshift;
       const size_t left = ntiles - (g << gshift);
       const unsigned in_group = (unsigned)(left < ((size_t)1 << gshift) ? left : ((size_t)1 << gshift));
-      const bool last = atomicAdd(&ticket[MC_ARRIVAL_LINE * g], 1u) == in_group - 1u;
-      if (last) __threadfence();  // acquire: the group's totals
-      role = last ? 1 : 0;
+      role = atomicAdd(&ticket[MC_ARRIVAL_LINE * g], (unsigned)cnt_t) + (unsigned)cnt_t == in_group ? 1 : 0;
     }
   }
   __syncthreads();
@@ -443,7 +469,11 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__re
 #pragma unroll
   for (unsigned k = 0; k < 8; ++k) {
     const size_t j = (size_t)threadIdx.x * K + k;
-    own[k] = (k < K && j < cnt) ? sums[g0 + j] : 0.0;
+    // agent-scope loads: the group's totals were stored by other workgroups of this launch
+    own[k] = (k < K && j < cnt) ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t *>(sums)
+                                                                                    + g0 + j, __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT))
+                                : 0.0;
   }
 #pragma unroll
   for (unsigned k = 0; k < 8; ++k) tsum += own[k];
@@ -465,17 +495,18 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__re
     run += own[k];
   }
   if (threadIdx.x == 0) {
-    gtot[g] = tot;
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(gtot) + g, __builtin_bit_cast(uint64_t, tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     ticket[MC_ARRIVAL_LINE * g] = 0;  // every arrival of the group is in
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned ngroups = (unsigned)((ntiles + ((size_t)1 << gshift) - 1) >> gshift);
     const bool last = atomicAdd(&ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS], 1u) == ngroups - 1u;
     if (last) {
-      __threadfence();
       double acc = 0.0;
       for (unsigned k = 0; k < ngroups; ++k) {
         gpre[k] = acc;
-        acc += gtot[k];
+        acc += __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t *>(gtot) + k,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       }
       ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS] = 0;
     }
@@ -1365,8 +1396,9 @@ static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws
     unsigned gshift = 8;  // >= MC_BLOCK tiles per group, at most FS_MAX_GROUPS groups
     while ((ntiles + ((size_t)1 << gshift) - 1) >> gshift > FS_MAX_GROUPS) ++gshift;
     fp = FsPre{pre, gpre, gshift};
-    k_fspec_reduce_g<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums, pre, gtot, gpre, tfail, fail,
-                                                                       ticket, ntiles, gshift);
+    const unsigned grid = (unsigned)((ntiles + FS_RG - 1) / FS_RG);
+    k_fspec_reduce_g<A_, D, SW><<<grid, MC_BLOCK, 0, st>>>(s, n, a, sums, pre, gtot, gpre, tfail, fail, ticket, ntiles,
+                                                           gshift);
   } else {
     k_fspec_reduce<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
     k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail,

@@ -152,6 +152,22 @@ def check_fso():
     return ok
 
 
+def check_bitround_shuffle():
+    """BitRound(k) + Shuffle(4) of one large chunk for every keepbits (each
+    plane split of the mask) against the oracle."""
+    from numcodecs_amd import BitRound, batch
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(8 << 20, generator=g, dtype=torch.float32)
+    xh = x.numpy()
+    xd = x.to(dev)
+    ok = True
+    for k in (0, 1, 7, 8, 9, 10, 15, 16, 22):
+        got = batch.FilterPipeline([BitRound(k), Shuffle(4)]).encode(xd)
+        ok &= _h(got) == oracle.shuffle(oracle.bitround_encode(xh, k), 4).tobytes()
+    return ok
+
+
 # field -> (alternative values, check)
 PLAN = {
     "copy_u": ([8], check_copy),
@@ -172,6 +188,7 @@ PLAN = {
     "fastdiv": ([0], check_fso),
     "crc_lds": ([1], check_checksums),
     "delta_enc_dv": ([8], check_delta_same_type),
+    "br_planes": ([0], check_bitround_shuffle),
 }
 
 

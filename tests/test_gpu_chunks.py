@@ -11,7 +11,7 @@ import torch
 import oracle
 from numcodecs_amd import (
     CRC32, CRC32C, Adler32, AsType, BitRound, Delta, FixedScaleOffset, Fletcher32, JenkinsLookup3,
-    PackBits, Quantize, Shuffle, batch, chunks,
+    PackBits, Quantize, Shuffle, batch, chunks, multi,
 )
 from tests import oracle_chain
 
@@ -340,15 +340,56 @@ def test_multi_device_decode_raises_first_mismatch(device):
 
 
 @pytest.mark.parametrize("es", [4, 8])
-def test_multi_device_host_pipeline_vs_oracle(device, es):
+def test_multi_device_host_pipeline_vs_oracle(device, es, monkeypatch):
     b, n = 13, 65536 + 16 * es
     g = torch.Generator().manual_seed(23)
     host_in = torch.randint(0, 256, (b, n), generator=g, dtype=torch.uint8).pin_memory()
     host_out = torch.empty_like(host_in).pin_memory()
+    runs = []
+    real = multi.run_workers
+    monkeypatch.setattr(multi, "run_workers", lambda fns: runs.append(len(fns)) or real(fns))
     batch.host_pipeline(host_in, host_out, es, encode=True, slice_chunks=3, devices=[device, device, device])
+    assert runs == [3], runs  # three workers, one per devices entry
     hi, ho = host_in.numpy(), host_out.numpy()
     for i in range(b):
         assert ho[i].tobytes() == oracle.shuffle(hi[i], es).tobytes(), i
     back = torch.empty_like(host_in).pin_memory()
     batch.host_pipeline(host_out, back, es, encode=False, slice_chunks=2, devices=[device, device])
     assert torch.equal(back, host_in)
+
+
+@pytest.mark.parametrize("name", ["bitround_shuffle_crc32", "fso_delta_shuffle_adler32"])
+def test_resident_shards_vs_oracle(device, name):
+    """Per-device resident shards (a list of device tensors; here both on the
+    box's one GPU): each shard encodes / decodes where it lives, results
+    left on its device, byte-identical to the oracle chain row by row."""
+    codecs, dtype = _chains()[name]
+    xs = [_make(dtype, b, 4096 + 32, device, 30 + b) for b in (5, 3)]
+    encs = chunks.encode_chunks(codecs, xs)
+    assert isinstance(encs, list) and len(encs) == 2
+    for x, e in zip(xs, encs):
+        assert e.device == x.device
+        eu = _rows_u8(e, x.shape[0])
+        xh = x.cpu().numpy()
+        for i in range(x.shape[0]):
+            assert eu[i].tobytes() == oracle_chain.chain_encode(codecs, xh[i]), (name, i)
+    decs = chunks.decode_chunks(codecs, encs)
+    for x, e, d in zip(xs, encs, decs):
+        du = _rows_u8(d, x.shape[0])
+        eu = _rows_u8(e, x.shape[0])
+        for i in range(x.shape[0]):
+            assert du[i].tobytes() == oracle_chain.chain_decode(codecs, eu[i].tobytes()), (name, i)
+    bad = [e.clone() for e in encs]
+    bad[1].view(torch.uint8)[2, 17] ^= 1
+    with pytest.raises(RuntimeError, match="checksum do not match"):
+        chunks.decode_chunks(codecs, bad)
+
+
+def test_one_device_batch_refuses_other_gpus(device):
+    """A batch on one GPU with devices naming another is refused (no silent
+    xGMI round trip); the same GPU repeated is the in-place partition."""
+    codecs, dtype = _chains()["bitround_shuffle_crc32"]
+    x = _make(dtype, 4, 4096, device, 40)
+    other = torch.device("cuda", device.index + 1)
+    with pytest.raises(ValueError, match="allow_peer_copy"):
+        chunks.encode_chunks(codecs, x, devices=[device, other])

@@ -56,3 +56,28 @@ def test_normalize_devices_rejects_cpu():
 
     assert multi.normalize_devices([0, "cuda:1", torch.device("cuda", 2)]) == [
         torch.device("cuda", 0), torch.device("cuda", 1), torch.device("cuda", 2)]
+
+
+def test_peer_devices_refused_unless_allowed():
+    """A one-device batch naming other GPUs is refused:
+    shipping rows over xGMI and back is opt-in; the batch's own GPU repeated
+    is the in-place partition."""
+    import torch
+
+    home = torch.device("cuda", 0)
+    assert multi.check_peer_devices(home, [home, home], False) is False
+    with pytest.raises(ValueError, match="allow_peer_copy"):
+        multi.check_peer_devices(home, [home, torch.device("cuda", 1)], False)
+    assert multi.check_peer_devices(home, [torch.device("cuda", 1)], True) is True
+
+
+def test_split_rows_partition_matches_shard():
+    """Every row in exactly one worker's range, in order (shard.chunk_range)."""
+    from numcodecs_amd import shard
+
+    for nrows in (0, 1, 7, 8, 8193):
+        for ndev in (1, 2, 3, 8):
+            parts = multi.split_rows(nrows, ndev)
+            rows = [r for _, lo, hi in parts for r in range(lo, hi)]
+            assert rows == list(range(nrows))
+            assert all(shard.chunk_range(nrows, g, ndev) == (lo, hi) for g, lo, hi in parts)

@@ -39,6 +39,7 @@ const field kFields[] = {
     {"fastdiv", "MCODEC_FASTDIV", &mc_sched.fastdiv},
     {"crc_lds", "MCODEC_CRC_LDS", &mc_sched.crc_lds},
     {"delta_enc_dv", "MCODEC_DELTA_ENC_DV", &mc_sched.delta_enc_dv},
+    {"br_planes", "MCODEC_BR_PLANES", &mc_sched.br_planes},
 };
 
 __attribute__((constructor)) void lab_sched_from_env() {
