@@ -359,22 +359,6 @@ MC_DEV uint64_t fs_wave_min_fail(uint64_t first) {
   return first;
 }
 
-// A tile's prefix (the double every candidate of the tile is offset by).
-// Two-launch decode (with an arrival ticket): the group's exclusive prefix of
-// the tile's group (gpre, <= 64 groups of 2^gshift tiles) plus the tile's
-// exclusive prefix inside its group (ipre), both written by the reduce pass's
-// last arrivers; one add, so every reader (apply pass, walker) rebuilds
-// bitwise the same value.  Without a ticket (HIP-graph capture): ipre is the
-// whole prefix (k_fspec_pre) and gpre is null.
-constexpr int FS_RG = 4;  // tiles per k_fspec_reduce_g workgroup (divides every group)
-
-struct FsPre {
-  const double *ipre;
-  const double *gpre;
-  unsigned gshift;
-  MC_DEV double at(size_t t) const { return gpre ? gpre[t >> gshift] + ipre[t] : ipre[t]; }
-};
-
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__restrict__ src, size_t n, int a,
                                                           double *__restrict__ sums) {
@@ -389,134 +373,28 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce(const uint8_t *__rest
   if (threadIdx.x == MC_BLOCK - 1) sums[blockIdx.x] = (double)p[FS_Q - 1][W - 1];
 }
 
-// Two-launch form (k_fspec_pre's launch folded in): as
-// k_fspec_reduce over FS_RG consecutive tiles per workgroup (one arrival per
-// FS_RG tiles: with one tile each, the 16 Ki returning arrivals of 256 MiB
-// f4 kept every workgroup alive an atomic round trip longer, 58 against
-// 44 us), and each tile also resets its failure word (tile 0 the
-// first-failure word) for the apply pass.  The workgroup then arrives on its
-// group's ticket word; the group's last arriver computes the group's
-// exclusive in-group prefixes (ipre) and total, and the last group to finish
-// scans the <= 64 group totals into gpre (fixed association throughout;
-// any association works, the apply pass only proposes candidates from them).
-// Ticket words are left zero.  Hand-offs inside the launch: every total is
-// an agent-scope (sc1) store drained by `s_waitcnt vmcnt(0)` before the
-// arrival, and the last arriver reads them with agent-scope loads
-// (MI355X_MICROARCH.md, correctness boundaries, the sc1 form).
-template <int A_, int D, int SW = 0>
-__global__ __launch_bounds__(MC_BLOCK) void k_fspec_reduce_g(const uint8_t *__restrict__ src, size_t n, int a,
-                                                            double *__restrict__ sums, double *__restrict__ ipre,
-                                                            double *__restrict__ gtot, double *__restrict__ gpre,
-                                                            uint64_t *__restrict__ tfail, uint64_t *__restrict__ fail,
-                                                            uint32_t *__restrict__ ticket, size_t ntiles,
-                                                            unsigned gshift) {
-  using Tr = FsT<A_, D>;
-  using P = typename Tr::P;
-  constexpr int W = Tr::W;
-  __shared__ P lds[FS_RG][FS_Q][MC_BLOCK / 64];
-  __shared__ double wsum[MC_BLOCK / 64];
-  __shared__ int role;  // 1: the last arrival of its group
-  const size_t tile = (size_t)blockIdx.x * FS_RG;  // this workgroup's first tile
-  const int cnt_t = (int)(ntiles - tile < (size_t)FS_RG ? ntiles - tile : (size_t)FS_RG);
-  {
-    typename Tr::V v[FS_RG][FS_Q][W];
-    if ((tile + FS_RG) * fs_tile<D>() <= n) {
-      // FS_RG whole tiles: every load issued before the first scan
-#pragma unroll
-      for (int r = 0; r < FS_RG; ++r) fs_load<A_, D, SW>(src, n, (tile + r) * fs_tile<D>(), a, v[r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < FS_RG; ++r)
-        if (r < cnt_t) fs_load<A_, D, SW>(src, n, (tile + r) * fs_tile<D>(), a, v[r]);
-    }
-    P tot[FS_RG];
-#pragma unroll
-    for (int r = 0; r < FS_RG; ++r) {
-      P p[FS_Q][W];
-      fs_tile_scan<typename Tr::V, W, P>(v[r], p, lds[r]);
-      tot[r] = p[FS_Q - 1][W - 1];
-    }
-    if (threadIdx.x == MC_BLOCK - 1) {
-      // the totals are handed to the group's last arriver inside this launch:
-      // agent-scope stores drained before the arrival (no release fence: an
-      // agent-scope fence writes back the XCD's L2 in every workgroup)
-#pragma unroll
-      for (int r = 0; r < FS_RG; ++r) {
-        if (r < cnt_t) {
-          __hip_atomic_store(reinterpret_cast<uint64_t *>(sums) + tile + r, __builtin_bit_cast(uint64_t, (double)tot[r]),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          tfail[tile + r] = ~(uint64_t)0;  // read by the next launch
-        }
-      }
-      if (tile == 0) *fail = n;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const size_t g = tile >> gshift;
-      const size_t left = ntiles - (g << gshift);
-      const unsigned in_group = (unsigned)(left < ((size_t)1 << gshift) ? left : ((size_t)1 << gshift));
-      role = atomicAdd(&ticket[MC_ARRIVAL_LINE * g], (unsigned)cnt_t) + (unsigned)cnt_t == in_group ? 1 : 0;
-    }
-  }
-  __syncthreads();
-  if (role == 0) return;
-  // the group's exclusive prefixes: thread t owns K = 2^gshift / MC_BLOCK
-  // consecutive tiles (sequential), then a block scan of the thread totals
-  const size_t g = tile >> gshift, g0 = g << gshift;
-  const size_t cnt = (ntiles - g0) < ((size_t)1 << gshift) ? (ntiles - g0) : ((size_t)1 << gshift);
-  const unsigned K = (1u << gshift) / MC_BLOCK;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double own[8];  // K <= 8 (at most 2048 tiles per group)
-  double tsum = 0.0;
-#pragma unroll
-  for (unsigned k = 0; k < 8; ++k) {
-    const size_t j = (size_t)threadIdx.x * K + k;
-    // agent-scope loads: the group's totals were stored by other workgroups of this launch
-    own[k] = (k < K && j < cnt) ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t *>(sums)
-                                                                                    + g0 + j, __ATOMIC_RELAXED,
-                                                                                __HIP_MEMORY_SCOPE_AGENT))
-                                : 0.0;
-  }
-#pragma unroll
-  for (unsigned k = 0; k < 8; ++k) tsum += own[k];
-  const double incl = mc_wave_scan_f64(tsum);
-  const double ex = mc_wave_shr1_f64(incl);
-  if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
-  double base = 0.0, tot = 0.0;
-#pragma unroll
-  for (int w = 0; w < MC_BLOCK / 64; ++w) {
-    if (w < wave) base += wsum[w];
-    tot += wsum[w];
-  }
-  double run = base + (lane ? ex : 0.0);
-#pragma unroll
-  for (unsigned k = 0; k < 8; ++k) {
-    const size_t j = (size_t)threadIdx.x * K + k;
-    if (k < K && j < cnt) ipre[g0 + j] = run;
-    run += own[k];
-  }
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(gtot) + g, __builtin_bit_cast(uint64_t, tot), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    ticket[MC_ARRIVAL_LINE * g] = 0;  // every arrival of the group is in
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned ngroups = (unsigned)((ntiles + ((size_t)1 << gshift) - 1) >> gshift);
-    const bool last = atomicAdd(&ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS], 1u) == ngroups - 1u;
-    if (last) {
-      double acc = 0.0;
-      for (unsigned k = 0; k < ngroups; ++k) {
-        gpre[k] = acc;
-        acc += __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t *>(gtot) + k,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      }
-      ticket[MC_ARRIVAL_LINE * MC_ARRIVAL_SHARDS] = 0;
-    }
-  }
-}
-
+// VERDICT r5 item 2 asked for k_fspec_pre's launch to be folded away, as the
+// integer scans fold theirs.  Four forms were built and measured against
+// this one on one box (256 MiB f4 of smooth data, the whole decode through
+// mc_delta_decode with and without a ticket, 7 interleaved rounds of 20
+// calls, tools/probe_fspec_fold.py, profiles/r06/probe_fspec_fold_*.json):
+//   * the reduce pass's last arrivers scan the tile totals (group words in
+//     the arrival ticket, sc1 hand-offs): 130.3 against 129.1 us -- every
+//     workgroup waits for its returning arrival, the reduce pass 44 -> 52.5;
+//   * the apply pass rebuilds its prefix from group accumulators (no-return
+//     float atomics in the ticket) and the earlier totals of its group:
+//     138.2 against 127.4 us -- two more dependent round trips per apply
+//     workgroup, the apply pass 78 -> 95.6;
+//   * k_fspec_pre over group accumulators (one workgroup per group, ~2 loads
+//     per thread: 4.8 instead of 6.5 us): 129.1 against 128.2 us -- the
+//     reduce pass's float atomics cost more (44 -> 49.6), also with the tiles
+//     permuted over the groups (50.5; 131.9 against 130.2).
+// None wins, so the decode keeps reduce -> k_fspec_pre -> apply -> walk.
 template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restrict__ src,
                                                          uint8_t *__restrict__ dst, size_t n, int a,
-                                                         const double *__restrict__ sums, FsPre pre_t,
+                                                         const double *__restrict__ sums,
+                                                         const double *__restrict__ pre_t,
                                                          uint64_t *__restrict__ tfail,
                                                          uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
@@ -535,7 +413,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   fs_load<A_, D, SW>(src, n, t0, a, v);
   P p[FS_Q][W];
   fs_tile_scan<typename Tr::V, W, P>(v, p, lds);
-  const P Sp = (P)pre_t.at(tile);  // the tile's prefix
+  const P Sp = (P)pre_t[tile];  // the tile's prefix
   S c[FS_Q][W], up[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -547,7 +425,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_apply(const uint8_t *__restr
   __syncthreads();
   // the tile's last candidate in the previous tile: the same double sum it
   // was rounded from there (sums[] is that tile's last prefix, bitwise)
-  const S pbound = tile ? Tr::bound(pre_t.at(tile - 1), sums[tile - 1]) : (S)0;
+  const S pbound = tile ? Tr::bound(pre_t[tile - 1], sums[tile - 1]) : (S)0;
   S p0[FS_Q];
 #pragma unroll
   for (int q = 0; q < FS_Q; ++q) {
@@ -1042,7 +920,8 @@ template <int A_, int D, int SW = 0>
 __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restrict__ src, size_t src_stride,
                                                         uint8_t *__restrict__ dst, size_t dst_stride, size_t n,
                                                         int a, uint64_t *__restrict__ rowfail,
-                                                        const double *__restrict__ sums, FsPre pre,
+                                                        const double *__restrict__ sums,
+                                                        const double *__restrict__ pre,
                                                         const uint64_t *__restrict__ tfail,
                                                         const uint64_t *__restrict__ fail) {
   using Tr = FsT<A_, D>;
@@ -1080,7 +959,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     if (f >= n) return;        // everything verified: dst is final
     t = (size_t)(f / TE);
     has_in = t > 0;
-    if (has_in) yin = Tr::bound(pre.at(t - 1), sums[t - 1]);  // tile t-1 verified: its last candidate
+    if (has_in) yin = Tr::bound(pre[t - 1], sums[t - 1]);  // tile t-1 verified: its last candidate
   } else {
     // a row that k_fspec_rows left at its first failing tile (rowfail = its
     // start; n when the row verified): resume there from the last stored value
@@ -1107,12 +986,12 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
       t = te;
       if (t >= ntiles) break;
       fsw_load<A_, D, SW>(src, n, t * (size_t)TE, a, nv);
-      if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre.at(t - 1), sums[t - 1]))) {
+      if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t - 1], sums[t - 1]))) {
         const size_t nt = fsw_next_failed(tfail, t, ntiles, ldsx);
         if (nt >= ntiles) break;
         if (nt != t) {
           t = nt;
-          yin = Tr::bound(pre.at(nt - 1), sums[nt - 1]);
+          yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
           fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         }
         serial_run = 0;
@@ -1299,13 +1178,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_walk(const uint8_t *__restri
     has_in = true;
     fsw_store<A_, D, SW>(dst, n, t0, c);
     if (t + 1 >= ntiles) break;
-    if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre.at(t), sums[t]))) {
+    if (single && Tr::bits(yin) == Tr::bits(Tr::bound(pre[t], sums[t]))) {
       // in sync with the apply pass: tiles that verified there are final
       const size_t nt = fsw_next_failed(tfail, t + 1, ntiles, ldsx);
       if (nt >= ntiles) break;
       if (nt != t + 1) {
         t = nt;
-        yin = Tr::bound(pre.at(nt - 1), sums[nt - 1]);
+        yin = Tr::bound(pre[nt - 1], sums[nt - 1]);
         fsw_load<A_, D, SW>(src, n, nt * (size_t)TE, a, nv);
         continue;
       }
@@ -1381,32 +1260,20 @@ __global__ __launch_bounds__(MC_BLOCK) void k_fspec_pre(const double *__restrict
   if (blockIdx.x == 0 && threadIdx.x == 0) *fail = n;
 }
 
-// Workspace (fspec_ws_bytes): sums, pre / ipre, tfail (ntiles words each),
-// 64 group totals, 64 group prefixes, then fail (the last word).  With an arrival ticket
-// the tile prefixes come out of the reduce pass (k_fspec_reduce_g: three
-// launches); without one (HIP-graph capture) k_fspec_pre computes them.
+// Workspace (fspec_ws_bytes): sums, pre, tfail (ntiles words each), then
+// fail (the last word).  `ticket` is unused: every arrival-ticket schedule
+// measured slower (above).
 template <int A_, int D, int SW = 0>
 static void launch_fspec(const uint8_t *s, uint8_t *d, size_t n, int a, void *ws, uint32_t *ticket, hipStream_t st) {
+  (void)ticket;
   const size_t ntiles = fspec_ntiles(n, D);
   double *sums = static_cast<double *>(ws), *pre = sums + ntiles;
-  uint64_t *tfail = reinterpret_cast<uint64_t *>(pre + ntiles), *fail = tfail + ntiles + 2 * FS_MAX_GROUPS;
-  double *gtot = reinterpret_cast<double *>(tfail + ntiles), *gpre = gtot + FS_MAX_GROUPS;
-  FsPre fp{pre, nullptr, 0};
-  if (ticket) {
-    unsigned gshift = 8;  // >= MC_BLOCK tiles per group, at most FS_MAX_GROUPS groups
-    while ((ntiles + ((size_t)1 << gshift) - 1) >> gshift > FS_MAX_GROUPS) ++gshift;
-    fp = FsPre{pre, gpre, gshift};
-    const unsigned grid = (unsigned)((ntiles + FS_RG - 1) / FS_RG);
-    k_fspec_reduce_g<A_, D, SW><<<grid, MC_BLOCK, 0, st>>>(s, n, a, sums, pre, gtot, gpre, tfail, fail, ticket, ntiles,
-                                                           gshift);
-  } else {
-    k_fspec_reduce<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
-    k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail,
-                                                                                     n);
-  }
-  k_fspec_apply<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, fp, tfail, fail);
+  uint64_t *tfail = reinterpret_cast<uint64_t *>(pre + ntiles), *fail = tfail + ntiles;
+  k_fspec_reduce<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, n, a, sums);
+  k_fspec_pre<<<(unsigned)((ntiles + MC_BLOCK - 1) / MC_BLOCK), MC_BLOCK, 0, st>>>(sums, pre, ntiles, tfail, fail, n);
+  k_fspec_apply<A_, D, SW><<<(unsigned)ntiles, MC_BLOCK, 0, st>>>(s, d, n, a, sums, pre, tfail, fail);
   // one walker from the first failing tile (returns at once if none failed)
-  k_fspec_walk<A_, D, SW><<<1, MC_BLOCK, 0, st>>>(s, 0, d, 0, n, a, nullptr, sums, fp, tfail, fail);
+  k_fspec_walk<A_, D, SW><<<1, MC_BLOCK, 0, st>>>(s, 0, d, 0, n, a, nullptr, sums, pre, tfail, fail);
 }
 
 // the speculative rows pass, then one walker per row that failed (rows that
@@ -1415,8 +1282,8 @@ template <int A_, int D, int SW = 0>
 static void launch_fspec_rows(const uint8_t *sc, size_t src_stride, uint8_t *dc, size_t dst_stride, size_t n, int a,
                               uint64_t *fail, unsigned g, hipStream_t st) {
   k_fspec_rows<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail);
-  k_fspec_walk<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr,
-                                                FsPre{nullptr, nullptr, 0}, nullptr, nullptr);
+  k_fspec_walk<A_, D, SW><<<g, MC_BLOCK, 0, st>>>(sc, src_stride, dc, dst_stride, n, a, fail, nullptr, nullptr,
+                                                nullptr, nullptr);
 }
 
 }  // namespace

@@ -477,12 +477,9 @@ static inline bool fspec_types_ok(int astype, int dtype) {
          mc_float_loop_dtype(astype, dtype) == mc_dt_base(dtype);
 }
 
-// tile totals, tile prefixes, per-tile first failures, group totals, group
-// prefixes, the first failure (the last word, read by the tests)
-constexpr size_t FS_MAX_GROUPS = 64;
-static inline size_t fspec_ws_bytes(size_t n, int dt) {
-  return (3 * fspec_ntiles(n, dt) + 1 + 2 * FS_MAX_GROUPS) * sizeof(uint64_t);
-}
+// tile totals, tile prefixes, per-tile first failures, the first failure
+// (the last word, read by the tests)
+static inline size_t fspec_ws_bytes(size_t n, int dt) { return (3 * fspec_ntiles(n, dt) + 1) * sizeof(uint64_t); }
 
 // speculative float Delta decode of one chunk (workspace fspec_ws_bytes) /
 // of `g` rows (fail: one word per row), output dtype f2 / f4 / f8, any

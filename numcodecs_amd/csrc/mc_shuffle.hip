@@ -840,12 +840,19 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     }
   }
   if constexpr (ES == 4 && BR) {
-    if (layout == (V_REG | V_BIG8) && mc_sched.br_planes) {  // C3: the mask applied per plane
+    if ((layout == (V_REG | V_BIG8) || layout == (V_REG | V_BIG4)) && mc_sched.br_planes) {
+      // C3: the mask applied per plane
       const int z = br.maskbits / 8;
       const uint32_t pmask = 0x01010101u * (uint32_t)((br.mask >> (8 * z)) & 0xffu);
-      if (z == 0) k_bitround_shuffle4_planes<0, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
-      else if (z == 1) k_bitround_shuffle4_planes<1, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
-      else k_bitround_shuffle4_planes<2, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+      if (layout & V_BIG8) {
+        if (z == 0) k_bitround_shuffle4_planes<0, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else if (z == 1) k_bitround_shuffle4_planes<1, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else k_bitround_shuffle4_planes<2, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+      } else {
+        if (z == 0) k_bitround_shuffle4_planes<0, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else if (z == 1) k_bitround_shuffle4_planes<1, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else k_bitround_shuffle4_planes<2, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+      }
       return;
     }
   }

@@ -151,9 +151,13 @@ def delta_decode_both_schedules(src, dst, n, a, d, ws_n):
     """mc_delta_decode of device bytes `src` into `dst` twice: with a fresh
     arrival ticket (the product's schedule: the float decode's tile prefixes
     folded into its reduce pass) and without one (the HIP-graph-capture
-    schedule, k_fspec_pre).  Both must give the same bytes and the same
-    first-failure word (the workspace's last word, returned; None without a
-    workspace); the ticket must be left zero."""
+    schedule, k_fspec_pre).  Both must give the same bytes (numpy's); the
+    ticket must be left zero.  The first-failure word (the workspace's last
+    word; the ticket schedule's is returned, None without a workspace) is
+    where the speculation's candidates first missed, and the two schedules
+    add the tile prefixes in different orders, so on inexact data they may
+    miss at different tiles -- but a chunk that verifies entirely under one
+    verifies under the other."""
     import torch
 
     from numcodecs_amd import _native, _ops
@@ -172,5 +176,5 @@ def delta_decode_both_schedules(src, dst, n, a, d, ws_n):
         out.append(dst.cpu().numpy().tobytes())
         words.append(int(ws[-1].item()) if ws_n else None)
     assert out[0] == out[1], "ticket / ticket-free schedules differ"
-    assert words[0] == words[1], words
+    assert (words[0] == n) == (words[1] == n), words
     return words[0]

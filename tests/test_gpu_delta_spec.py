@@ -59,8 +59,8 @@ def _decode_raw(enc_np, dt):
     a = _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, a)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    # totals, prefixes, per-tile failures, 64 group totals / prefixes, first failure
-    assert ws_n == (3 * ntiles + 1 + 128) * 8
+    # totals, prefixes, per-tile failures, first failure
+    assert ws_n == (3 * ntiles + 1) * 8
     first = delta_decode_both_schedules(src, dst, n, a, a, ws_n)
     return dst.cpu().numpy(), first
 

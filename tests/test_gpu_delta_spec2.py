@@ -51,7 +51,7 @@ def _decode_raw(enc_np, dt, at):
     a, d = _ops.dtype_code(at), _ops.dtype_code(dt)
     ws_n = _native.lib.mc_delta_decode_workspace(n, a, d)
     ntiles = (n + _tile(dt) - 1) // _tile(dt)
-    assert ws_n == ((3 * ntiles + 1 + 128) * 8 if _speculative(dt, at) else 0)
+    assert ws_n == ((3 * ntiles + 1) * 8 if _speculative(dt, at) else 0)
     first = delta_decode_both_schedules(src, dst, n, a, d, ws_n)
     return dst.cpu().numpy().view(np.dtype(dt)), first
 
