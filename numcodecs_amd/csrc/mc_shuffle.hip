@@ -840,7 +840,8 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
     }
   }
   if constexpr (ES == 4 && BR) {
-    if ((layout == (V_REG | V_BIG8) || layout == (V_REG | V_BIG4)) && mc_sched.br_planes) {
+    if ((layout == (V_REG | V_BIG8) || layout == (V_REG | V_BIG4) || layout == (V_REG | V_BIG)) &&
+        mc_sched.br_planes) {
       // C3: the mask applied per plane
       const int z = br.maskbits / 8;
       const uint32_t pmask = 0x01010101u * (uint32_t)((br.mask >> (8 * z)) & 0xffu);
@@ -848,10 +849,14 @@ static void launch_enc_nt(int layout, const uint8_t *s, uint8_t *d, const ChunkM
         if (z == 0) k_bitround_shuffle4_planes<0, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
         else if (z == 1) k_bitround_shuffle4_planes<1, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
         else k_bitround_shuffle4_planes<2, NT, 8><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
-      } else {
+      } else if (layout & V_BIG4) {
         if (z == 0) k_bitround_shuffle4_planes<0, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
         else if (z == 1) k_bitround_shuffle4_planes<1, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
         else k_bitround_shuffle4_planes<2, NT, 4><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+      } else {
+        if (z == 0) k_bitround_shuffle4_planes<0, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else if (z == 1) k_bitround_shuffle4_planes<1, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
+        else k_bitround_shuffle4_planes<2, NT, 2><<<grid, MC_BLOCK, 0, st>>>(s, d, m, ntiles, br, pmask);
       }
       return;
     }
@@ -992,6 +997,13 @@ int mc_shuffle_impl(const void *src_, size_t src_stride, void *dst_, size_t dst_
   unsigned default_cap = MC_MAX_GRID;
   if (variant == V_DEFAULT) {
     variant = default_variant(es, enc, chunk_bytes * nchunks, m.count, nchunks, &default_cap);
+    // BitRound + Shuffle(4) of a large chunk: the plane-masked kernel on 64
+    // KiB tiles (half the registers of the 128 KiB tiles, twice the waves to
+    // hide its BitRound VALU): 256 MiB 89.2-89.4 against 89.7-91.0 us for
+    // 128 KiB tiles, 91.3-92.2 for the element-masked kernel, plain
+    // Shuffle(4) 87.2-87.6 (profiles/r06/probe_c3_layouts*.json)
+    if (br && es == 4 && variant == (V_REG | V_BIG8) && tile_flag(m.count, 4096, V_BIG4) == V_BIG4)
+      variant = V_REG | V_BIG4;
     if (max_blocks <= 0) max_blocks = (int)default_cap;
   }
   const bool fast_es = es == 2 || es == 4 || es == 8 || es == 16;

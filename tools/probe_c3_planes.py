@@ -69,7 +69,8 @@ def main():
     lab_var.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                         ctypes.c_int, ctypes.c_void_p]
     lab_var.restype = ctypes.c_int
-    variants = {"reg_128k": 513, "reg_64k": 129, "pipe_64k": 385, "wide_64k": 134, "pair_128k": 517}
+    variants = {"reg_128k": 513, "reg_64k": 129, "reg_32k": 17, "reg_64k_g2": 129 | 32, "pipe_64k": 385,
+                "pair_128k": 517}
     for name, v in variants.items():
         def fn(i, v=v):
             assert lab_var(xs[i].data_ptr(), ys[i].data_ptr(), n, 4, 10, v, 0, st) == 0
