@@ -716,35 +716,47 @@ __global__ __launch_bounds__(MC_BLOCK) void k_bswap16(const uint8_t *__restrict_
 // ---------------------------------------------------------------------------
 // Delta decode with a longdouble loop (np.cumsum(enc, out=dec) accumulates in
 // promote(astype, dtype) = longdouble when either side is '<f16', delta.py:80):
-// one x87 add per element in numpy's left-to-right order, one workgroup.
-// Each batch of LDC_N elements is cast to longdouble by all threads into LDS,
-// thread 0 runs the chain over it, and all threads cast the running sums to
-// dtype and store them.  The first sum is the first element itself (numpy's
-// accumulate copies it).
+// one x87 add per element in numpy's left-to-right order, in ONE wave.  Each
+// lane casts one element of a 64-element batch to longdouble (the next
+// batch's loads are issued before this batch's chain); the chain reads lane
+// j's operand with v_readlane, so the running sum is wave-uniform and the
+// x87 add runs on the scalar unit (64-bit SALU shifts / adds / compares, one
+// issue per cycle, against ~4-8 cycles per dependent vector instruction of a
+// lane-0 chain), and lane j keeps sum j (a select); then every lane casts
+// and stores its sum.  The first sum is the first element
+// itself (numpy's accumulate copies it).
 // ---------------------------------------------------------------------------
-constexpr int LDC_N = 4 * MC_BLOCK;
+MC_DEV uint64_t x_readlane64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+  return ((uint64_t)hi << 32) | lo;
+}
 
-__global__ __launch_bounds__(MC_BLOCK) void k_ld_chain(const uint8_t *__restrict__ src, int a,
-                                                      uint8_t *__restrict__ dst, int d, size_t n, bool al) {
-  __shared__ X80 buf[LDC_N];
+__global__ __launch_bounds__(64) void k_ld_chain(const uint8_t *__restrict__ src, int a, uint8_t *__restrict__ dst,
+                                                 int d, size_t n, bool al) {
+  const int lane = threadIdx.x;
+  auto load = [&](size_t b0) -> X80 {
+    X80 re = x80_zero(0), im;
+    if (b0 + lane < n) x_to_x80(x_load(src, b0 + lane, a, al), a, re, im);
+    return re;
+  };
   X80 sum = x80_zero(0);
-  for (size_t b0 = 0; b0 < n; b0 += LDC_N) {
-    const int cnt = (int)(n - b0 < (size_t)LDC_N ? n - b0 : (size_t)LDC_N);
-    for (int j = threadIdx.x; j < cnt; j += MC_BLOCK) {
-      X80 re, im;
-      x_to_x80(x_load(src, b0 + j, a, al), a, re, im);
-      buf[j] = re;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int j = 0; j < cnt; ++j) {
-        sum = (b0 == 0 && j == 0) ? buf[j] : x80_add(sum, buf[j]);
-        buf[j] = sum;
+  X80 cur = load(0);
+  for (size_t b0 = 0; b0 < n; b0 += 64) {
+    const X80 nxt = load(b0 + 64);  // in flight during this batch's chain
+    const int cnt = (int)(n - b0 < 64 ? n - b0 : 64);
+    uint64_t rm = 0;
+    uint32_t rse = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const X80 x = x80_make(x_readlane64(cur.m, j), (uint32_t)__builtin_amdgcn_readlane((int)cur.se, j));
+      sum = (b0 == 0 && j == 0) ? x : x80_add(sum, x);
+      if (lane == j) {  // the sum into lane j (a select off the scalar chain)
+        rm = sum.m;
+        rse = sum.se;
       }
     }
-    __syncthreads();
-    for (int j = threadIdx.x; j < cnt; j += MC_BLOCK) x_store(dst, b0 + j, d, x_from_x80(buf[j], x80_zero(0), d), al);
-    __syncthreads();
+    if (lane < cnt) x_store(dst, b0 + lane, d, x_from_x80(x80_make(rm, rse), x80_zero(0), d), al);
+    cur = nxt;
   }
 }
 
@@ -876,8 +888,8 @@ int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dt
   if (ld_pair(astype, dtype)) {  // no workspace
     if (n == 0) return MC_OK;
     if (!src || !dst) return MC_EINVAL;
-    k_ld_chain<<<1, MC_BLOCK, 0, st>>>(static_cast<const uint8_t *>(src), astype, static_cast<uint8_t *>(dst), dtype,
-                                       n, x_aligned(src, astype) && x_aligned(dst, dtype));
+    k_ld_chain<<<1, 64, 0, st>>>(static_cast<const uint8_t *>(src), astype, static_cast<uint8_t *>(dst), dtype, n,
+                                 x_aligned(src, astype) && x_aligned(dst, dtype));
     return mc_last_launch();
   }
   const bool td = td_pair(astype, dtype), cx = cx_pair(astype, dtype);

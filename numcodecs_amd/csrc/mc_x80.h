@@ -141,6 +141,62 @@ MC_X80_FN int x80_eexp(X80 a) {
 
 // a + (negate_b ? -b : b)
 MC_X80_FN X80 x80_addsub(X80 a, X80 b, bool negate_b) {
+  // fast path: both operands normal (J set, exponent 1 .. 0x7ffe), exponent
+  // gap <= 63 or > 65, normal result -- the running sums of a Delta decode
+  // almost always; everything else takes the general code below (the same
+  // results: tests/test_x80.py)
+  {
+    const uint32_t ea0 = a.se & 0x7fffu, eb0 = b.se & 0x7fffu;
+    if (ea0 - 1u < 0x7ffeu && eb0 - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63)) {
+      uint32_t s1 = x80_sign(a), s2 = x80_sign(b) ^ (negate_b ? 1u : 0u);
+      uint32_t e1 = ea0, e2 = eb0;
+      uint64_t m1 = a.m, m2 = b.m;
+      if (e1 < e2 || (e1 == e2 && m1 < m2)) {
+        const uint32_t te = e1; e1 = e2; e2 = te;
+        const uint64_t tm = m1; m1 = m2; m2 = tm;
+        const uint32_t ts = s1; s1 = s2; s2 = ts;
+      }
+      const uint32_t d = e1 - e2;
+      if (d > 65u) return x80_make(m1, (s1 << 15) | e1);  // |smaller| < half an ulp
+      if (d <= 63u) {
+        const uint64_t bh = m2 >> d, bl = d ? m2 << (64u - d) : 0;
+        uint64_t hi, lo;
+        int e = (int)e1;
+        if (s1 == s2) {
+          hi = m1 + bh;
+          lo = bl;
+          if (hi < m1) {  // carry out: shift the 129-bit sum right by one
+            lo = (hi << 63) | (lo >> 1) | (lo & 1u);
+            hi = X80_J | (hi >> 1);
+            ++e;
+          }
+        } else {
+          lo = 0 - bl;
+          hi = m1 - bh - (bl != 0 ? 1u : 0u);
+          if (hi == 0 && lo == 0) return x80_zero(0);
+          const int k = hi ? x80_clz64(hi) : 64 + x80_clz64(lo);
+          if (e - k < 1) goto general;  // a denormal result
+          if (k >= 64) {
+            hi = lo << (k - 64);
+            lo = 0;
+          } else if (k) {
+            hi = (hi << k) | (lo >> (64 - k));
+            lo <<= k;
+          }
+          e -= k;
+        }
+        if ((lo >> 63) && ((lo << 1) != 0 || (hi & 1u))) {
+          if (++hi == 0) {
+            hi = X80_J;
+            ++e;
+          }
+        }
+        if (e >= 0x7fff) return x80_inf(s1);
+        return x80_make(hi, (s1 << 15) | (uint32_t)e);
+      }
+    }
+  }
+general:
   const int ca = x80_class(a), cb = x80_class(b);
   if (ca == X80_BAD || cb == X80_BAD) return x80_indefinite();
   if (x80_is_nan_class(ca) || x80_is_nan_class(cb)) return x80_nan2(a, ca, b, cb);
