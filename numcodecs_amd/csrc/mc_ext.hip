@@ -508,6 +508,10 @@ MC_DEV bool x_is_nan_bits(uint64_t b, int c) {
   }
 }
 
+// element i of the NaN-fix input plane as native bits (a real astype may be
+// big-endian: ADVICE r5, the raw bits missed its NaNs)
+MC_DEV uint64_t nf_load(const uint8_t *in, size_t i, int es, int ac) { return mc_to_storage(mc_load_elem(in, i, es), ac); }
+
 __global__ __launch_bounds__(MC_BLOCK) void k_nanfix_last(const uint8_t *__restrict__ in, int ac, size_t n,
                                                          long long *__restrict__ last) {
   __shared__ long long red[MC_BLOCK / 64];
@@ -515,7 +519,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_nanfix_last(const uint8_t *__restr
   const int es = mc_itemsize(ac);
   long long m = -1;
   for (size_t i = b0 + threadIdx.x; i < n && i < b0 + NF_BLOCK; i += MC_BLOCK)
-    if (x_is_nan_bits(mc_load_elem(in, i, es), ac)) m = (long long)i;
+    if (x_is_nan_bits(nf_load(in, i, es, ac), ac)) m = (long long)i;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const long long o = __shfl_xor(m, off);
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(MC_BLOCK) void k_nanfix_apply(const uint8_t *__rest
   const size_t e0 = b0 + (size_t)threadIdx.x * PER;
   long long mine = -1;
   for (int k = 0; k < PER; ++k)
-    if (e0 + k < n && x_is_nan_bits(mc_load_elem(in, e0 + k, es), ac)) mine = (long long)(e0 + k);
+    if (e0 + k < n && x_is_nan_bits(nf_load(in, e0 + k, es, ac), ac)) mine = (long long)(e0 + k);
   // exclusive prefix max over the block's threads: wave scan + wave totals
   long long incl = mine;
 #pragma unroll
@@ -581,13 +585,13 @@ __global__ __launch_bounds__(MC_BLOCK) void k_nanfix_apply(const uint8_t *__rest
   for (int k = 0; k < PER; ++k) {
     const size_t i = e0 + k;
     if (i >= n) break;
-    const uint64_t e = mc_load_elem(in, i, es);
+    const uint64_t e = nf_load(in, i, es, ac);
     if (x_is_nan_bits(e, ac)) j = (long long)i;
     if (j < 0) continue;
     const uint64_t sb = mc_load_elem(out, i, os);
     if (!x_is_nan_bits(sb, lc)) continue;
     // the NaN input at j in the loop type, quieted (numpy's cast then add)
-    const uint64_t eb = mc_load_elem(in, (size_t)j, es);
+    const uint64_t eb = nf_load(in, (size_t)j, es, ac);
     uint64_t v;
     if (mc_dt_base(lc) == MC_F4) {
       const uint32_t f = mc_dt_base(ac) == MC_F2 ? mc_half_to_float_bits((uint16_t)eb) : (uint32_t)eb;
@@ -854,6 +858,19 @@ static bool ld_pair(int astype, int dtype) {
   return x_is_ld(astype) || x_is_ld(dtype);
 }
 
+// numpy's NaN + NaN operand choice in the complex cumsum loops (see
+// k_nanfix_*): the SECOND operand's NaN for complex64 (complex128 when the
+// accumulate has exactly 2 elements), the first for complex128 -- measured on
+// the reference's numpy 2.2.6 on the x86-64 (AVX-512) host that made
+// tests/golden/ext.npz, i.e. numpy's SIMD dispatch there; another dispatch
+// could choose differently, so this rule's parity is pinned to those goldens
+// only.  clongdouble adds are x87 adds, whose NaN choice the real
+// chain already makes.
+static bool x_complex_cumsum_keeps_second_nan(int lc, size_t n) {
+  if (lc == MC_F16L) return false;
+  return (lc == MC_F4) != (n == 2);
+}
+
 static int nanfix(const uint8_t *in, int ac, uint8_t *out, int lc, size_t n, long long *last, long long *carry,
                   hipStream_t st) {
   const size_t nb = (n + NF_BLOCK - 1) / NF_BLOCK;
@@ -936,9 +953,7 @@ int mc_ext_delta_decode(const void *src, void *dst, size_t n, int astype, int dt
   off += 2 * x_align_up(n * lcs);
   uint8_t *rws = ws + off;
   const size_t rws_bytes = workspace_bytes - off;
-  // numpy's NaN + NaN operand choice of the complex loop (see k_nanfix_*)
-  // (clongdouble adds are x87 adds, whose NaN choice the real chain makes)
-  const bool second = lc != MC_F16L && ((lc == MC_F4) != (n == 2));
+  const bool second = x_complex_cumsum_keeps_second_nan(lc, n);
   const size_t nb = (n + NF_BLOCK - 1) / NF_BLOCK;
   long long *nf_last = reinterpret_cast<long long *>(rws), *nf_carry = nf_last + nb;
   int rc = mc_delta_decode(in_re, out_re, n, ac, lc, rws, rws_bytes, nullptr, st);

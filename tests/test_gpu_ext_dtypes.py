@@ -242,3 +242,24 @@ def test_delta_decode_first_element_nan_payload(device, t):
             want = np.cumsum(enc, out=np.empty(len(enc), dtype=dt)).tobytes()
         got = Delta(dtype=dt, astype=at).decode(enc)
         assert raw(got) == want, (at, dt)
+
+
+@pytest.mark.parametrize("at", ["<f4", ">f4", ">f2", "<f2", ">f8"])
+def test_complex_decode_from_real_astype_with_nans(device, at):
+    """Delta(complex64, astype=a real float of either byte order) decode of
+    data with NaNs (a big-endian astype's NaN inputs were tested
+    on their raw bytes): bytes identical to numpy's cumsum (the reference's
+    delta.py:80), computed on the host beside the run.  numpy's complex NaN
+    choice is pinned to the goldens' numpy (mc_ext.hip
+    x_complex_cumsum_keeps_second_nan)."""
+    n = 5000
+    rng = np.random.default_rng(8)
+    x = (rng.standard_normal(n) * 10).astype(np.dtype(at).newbyteorder("="))
+    x[[3, 17, 1000, 1001, 4000]] = np.nan
+    x[[50, 2000]] = [np.inf, -np.inf]
+    enc = x.astype(at)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want = np.cumsum(enc, out=np.empty(n, "<c8")).tobytes()
+    got = Delta(dtype="<c8", astype=at).decode(enc)
+    assert raw(got) == want
