@@ -543,7 +543,7 @@ def config_workloads(dev, cpu, sets: int = 4) -> dict:
     t_e = _timed(lambda i: pipe.encode(x32[i]), sets, 20)
     t_d = _timed(lambda i: sh4.decode(enc[i], out=dec[i]), sets, 20)
     out["cfg_C3"] = _cfg(2 * CHUNK / GiB / (t_e + t_d), t_e, t_d, 4 * CHUNK,
-                         "k_shuffle_enc<4,bitround> / k_shuffle4_dec_pair", cpu, "C3")
+                         "k_bitround_shuffle4_planes / k_shuffle4_dec_pair", cpu, "C3")
     del x32, enc, dec
     # C4 FSO(f4->i2) -> Delta(i2) -> Shuffle(2), fused kernels
     xc = [1000.0 + 10.0 * torch.rand(CHUNK // 4, device=dev) for _ in range(sets)]
@@ -648,7 +648,7 @@ def end_to_end(dev, cpu, total_gib: int = 1, chunk_bytes: int = 4 * MiB) -> dict
 def copy_ceiling(dev, nbytes: int = GiB, reps: int = 10) -> dict:
     """SURVEY §8d's "achievable" line, measured in this run: hipMemcpyAsync
     DtoD (torch's copy_) and libmcodec's nontemporal copy kernel (mc_copy) on
-    1 GiB, and the copy calibration of tools/lab/lab_bw.hip (plain 16-B/lane
+    1 GiB, and the copy calibration of tools/lab/lab_bw.hip (libmcodec_bwcal.so; plain 16-B/lane
     copies, nontemporal loads + stores, the layouts that stream fastest:
     8 vectors per thread one tile per workgroup, 4 per thread on a
     8192-workgroup grid) on 1 GiB and on 4 rotating 256 MiB sets -- the
@@ -682,23 +682,23 @@ def copy_ceiling(dev, nbytes: int = GiB, reps: int = 10) -> dict:
 
     res = {"hipMemcpyDtoD_1GiB_GBps": rate(lambda i: b.copy_(a), nbytes),
            "mc_copy_1GiB_GBps": rate(lambda i: _ops.copy(a, b, nbytes), nbytes)}
+    ins = [a[k * CHUNK:(k + 1) * CHUNK] for k in range(4)]
+    outs = [b[k * CHUNK:(k + 1) * CHUNK] for k in range(4)]
+    res["mc_copy_256MiB_rot4_GBps"] = rate(lambda i: _ops.copy(ins[i], outs[i], CHUNK), CHUNK, 4)
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from lab.lablib import lab as _lab
+        from lab.lablib import bwcal
 
-        lab = _lab()
+        lab = bwcal()
         for u, g in ((8, 0), (4, 8192)):
             res[f"nt_copy_u{u}_g{g}_1GiB_GBps"] = rate(
                 lambda i: lab.mc_lab_bw_copy(a.data_ptr(), b.data_ptr(), nbytes, u, g, 3, st), nbytes)
-        ins = [a[k * CHUNK:(k + 1) * CHUNK] for k in range(4)]
-        outs = [b[k * CHUNK:(k + 1) * CHUNK] for k in range(4)]
         for u, g in ((8, 0), (4, 8192)):
             res[f"nt_copy_u{u}_g{g}_256MiB_rot4_GBps"] = rate(
                 lambda i: lab.mc_lab_bw_copy(ins[i].data_ptr(), outs[i].data_ptr(), CHUNK, u, g, 3, st), CHUNK, 4)
-        res["mc_copy_256MiB_rot4_GBps"] = rate(lambda i: _ops.copy(ins[i], outs[i], CHUNK), CHUNK, 4)
-    except (ImportError, OSError, FileNotFoundError) as e:  # the lab library is optional
+    except (ImportError, OSError, FileNotFoundError) as e:  # built by __graft_entry__.build()
         res["nt_copy_calibration"] = f"unavailable: {e}"
-    del a, b
+    del a, b, ins, outs
     torch.cuda.empty_cache()
     res["ceiling_GBps"] = max(v for k, v in res.items() if k.endswith("_GBps"))
     return res

@@ -36,6 +36,24 @@ _SIGS = {
     "mc_lab_crc_product": ([_I, _V, _S, _I, ctypes.c_uint, _V, _V], _I),
 }
 _lib = None
+_bwcal = None
+BWCAL_PATH = os.path.join(os.path.dirname(LAB_PATH), "libmcodec_bwcal.so")
+
+
+def bwcal():
+    """The copy calibration alone (`make -C tools/lab bwcal`: lab_bw.hip, the
+    one lab entry bench.py's copy ceiling needs; it travels to the GPU box,
+    the full lab library does not)."""
+    global _bwcal
+    if _bwcal is None:
+        if not os.path.exists(BWCAL_PATH):
+            raise FileNotFoundError(f"{BWCAL_PATH} missing: build it with `make -C tools/lab bwcal`")
+        lib = ctypes.CDLL(BWCAL_PATH)
+        args, res = _SIGS["mc_lab_bw_copy"]
+        lib.mc_lab_bw_copy.argtypes = args
+        lib.mc_lab_bw_copy.restype = res
+        _bwcal = lib
+    return _bwcal
 
 
 def lab():
