@@ -609,23 +609,26 @@ def checksum32(kind, src, src_stride, nchunks, nbytes, init, prefix=None) -> tor
     return out[:nchunks]
 
 
-# Single-chunk Checksum32 encodes below this size finish in the tiles launch
-# (one launch: 1 MiB CRC32 / Adler32 encode 14.2 / 14.5 -> 10.5 / 8.3 us per
-# call); larger ones keep the separate finalize kernel, which measured ~3 us
-# faster on the GPU at 256 MiB (CRC32 99.9 vs 101.7-103.1 us: every block of
-# the fused copy drains its payload stores before it arrives).
+# Single-chunk Checksum32 encodes finish in the tiles launch (one launch: 1 MiB
+# CRC32 / Adler32 encode 14.2 / 14.5 -> 10.5 / 8.3 us per call).  CRC32 /
+# CRC32C at every size since round 6 (the workgroups' sums ride the arrival
+# atomics, ck_ride_arrive: 256 MiB 85.8 / 87.7 us against 93.9 / 90.6 for
+# tiles + finalize, tools/probe_ck_stamp.py); Adler32 below this size only
+# (at 256 MiB its separate finalize kernel measured ~3 us faster: every
+# block of the fused copy drains its payload stores before it arrives).
 _CK_FUSED_ENCODE_MAX = 16 << 20
 
 
 def checksum32_encode(kind, src, src_stride, dst, dst_stride, nchunks, nbytes, init, location,
                       prefix=None) -> None:
     """Checksum32.encode of `nchunks` rows into dst rows (LE32 footer at the start or end).
-    One chunk of CRC32 / CRC32C / Adler32 below _CK_FUSED_ENCODE_MAX runs in one
-    launch (the stream's arrival ticket; the tiles-then-finalize schedule
-    during HIP-graph capture and for larger chunks)."""
+    One chunk of CRC32 / CRC32C (Adler32 below _CK_FUSED_ENCODE_MAX) runs in
+    one launch (the stream's arrival ticket; the tiles-then-finalize schedule
+    during HIP-graph capture and for larger Adler32 chunks)."""
     _native.require_device()
     with _guard(src):
-        if nchunks == 1 and kind != _native.MC_CK_JENKINS and nbytes < _CK_FUSED_ENCODE_MAX:
+        if nchunks == 1 and kind != _native.MC_CK_JENKINS and (kind != _native.MC_CK_ADLER32
+                                                               or nbytes < _CK_FUSED_ENCODE_MAX):
             st = stream(src)
             sl = _verify_slot(src, st)
             if sl is not None:

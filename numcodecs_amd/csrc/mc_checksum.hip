@@ -372,6 +372,14 @@ inline unsigned ck_grid_cap_bs(bool copy) {
   return g > 0 ? (unsigned)g : 2048u;
 }
 
+// the bit-sliced kernel's grid; its one-launch finish (ck_ride_arrive) takes
+// at most CK_RIDE_MAX_GRID workgroups
+inline unsigned ck_bs_grid(size_t total, bool copy, bool fused) {
+  unsigned cap = ck_grid_cap_bs(copy);
+  if (fused && cap > CK_RIDE_MAX_GRID) cap = CK_RIDE_MAX_GRID;
+  return (unsigned)(total < cap ? total : cap);
+}
+
 // tile size (in STEP units) for a chunk: K = 1 below 64 KiB
 inline int ck_k(size_t n, bool copy) {
   return n < (size_t)16 * STEP ? 1 : copy ? ck_kcopy() : ck_kbig();
@@ -411,8 +419,7 @@ void dispatch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n
   const size_t total = tpc * nchunks;
   const int als = align_class(s, ss, nchunks);
   if (KIND != K_ADLER && K >= 4 && !mc_sched.crc_lds) {  // bit-sliced fold, persistent pipelined grid
-    const unsigned cap = ck_grid_cap_bs(d != nullptr);
-    const unsigned grid = (unsigned)(total < cap ? total : cap);
+    const unsigned grid = ck_bs_grid(total, d != nullptr, fx != nullptr);
     launch_crc_bs(KIND, K, als, d ? align_class(d, ds, nchunks) : 2, s, ss, d, ds, n, tpc, total, parts, fin, fx,
                   grid, st);
     return;
@@ -450,9 +457,10 @@ struct HostPow {
   }
 };
 
-// n: bytes the tiles cover; np: payload bytes (n - 4 with a head, else n)
+// n: bytes the tiles cover; np: payload bytes (n - 4 with a head, else n);
+// G: the bit-sliced kernel's grid (its one-launch finish)
 template <int KIND>
-CrcFin crc_fin_build(int K, size_t tpc, size_t n, size_t np) {
+CrcFin crc_fin_build(int K, size_t tpc, size_t n, size_t np, unsigned G) {
   CrcFin f{};
   f.head = n != np;
   if constexpr (KIND != K_ADLER) {
@@ -480,6 +488,9 @@ CrcFin crc_fin_build(int K, size_t tpc, size_t n, size_t np) {
     }
     f.pad = HostPow::pw(hp.x2n_inv, 8 * (tb * tpc - n), poly);
     f.xn = HostPow::pw(hp.x2n, 8 * (uint64_t)np, poly);
+    const uint32_t xg = xpow(G);
+    for (int m = 0; m < 32; ++m) f.xgb[m] = gf_mul(1u << m, xg, poly);
+    f.xh = HostPow::pw(hp.x2n, 8 * (uint64_t)np + 32, poly);
   }
   return f;
 }
@@ -487,18 +498,20 @@ CrcFin crc_fin_build(int K, size_t tpc, size_t n, size_t np) {
 // the constants of the last call on this thread (a stream of equal-size
 // chunks asks for the same ones every time)
 template <int KIND>
-const CrcFin &crc_fin(int K, size_t tpc, size_t n, size_t np) {
+const CrcFin &crc_fin(int K, size_t tpc, size_t n, size_t np, unsigned G) {
   thread_local struct {
     int K = -1;
     size_t tpc = 0, n = 0, np = 0;
+    unsigned G = 0;
     CrcFin f;
   } last;
-  if (KIND != K_ADLER && (last.K != K || last.tpc != tpc || last.n != n || last.np != np)) {
-    last.f = crc_fin_build<KIND>(K, tpc, n, np);
+  if (KIND != K_ADLER && (last.K != K || last.tpc != tpc || last.n != n || last.np != np || last.G != G)) {
+    last.f = crc_fin_build<KIND>(K, tpc, n, np, G);
     last.K = K;
     last.tpc = tpc;
     last.n = n;
     last.np = np;
+    last.G = G;
   }
   return last.f;
 }
@@ -519,11 +532,13 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   uint32_t *parts = static_cast<uint32_t *>(ws);
   // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
   const bool fused = ticket && nchunks == 1;
-  const CkFinish fx{init, seq, head, ticket, out, stored_out, footer, fs, stored};
+  CkFinish fx{init, seq, head, ticket, out, stored_out, footer, fs, stored, 0};
+  const unsigned G = ck_bs_grid(tpc * nchunks, d != nullptr, fused);
   switch (K) {
 #define MC_CK_CASE(KK)                                                                         \
   case KK: {                                                                                   \
-    const CrcFin &fin = crc_fin<KIND>(KK, tpc, n, np);                                         \
+    const CrcFin &fin = crc_fin<KIND>(KK, tpc, n, np, G);                                      \
+    if constexpr (KIND != K_ADLER) fx.c0 = gf_mul(~init, fin.xn, crc_poly<KIND>());            \
     dispatch_tiles<KIND, KK>(s, ss, d, ds, nchunks, n, tpc, parts, fin, fused ? &fx : nullptr, st); \
     if (!fused)                                                                                \
       k_ck_finalize<KIND, KK><<<(unsigned)nchunks, MC_BLOCK, 0, st>>>(                         \

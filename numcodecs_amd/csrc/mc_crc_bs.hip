@@ -4,6 +4,33 @@
 #include "mc_checksum.h"
 
 namespace mcck {
+// X^e, X = x^(8 * K * STEP), for e < CK_RIDE_MAX_GRID: the one-launch
+// finish's shift of workgroup b's last tile to the chunk end, e = (tiles - 1
+// - b) mod G (built by the compiler, one table per CRC and tile size)
+struct CkRidePow {
+  uint32_t p[CK_RIDE_MAX_GRID];
+};
+constexpr CkRidePow make_ride_pow(uint32_t poly, int K) {
+  CkRidePow t{};
+  uint32_t x2n[64] = {};
+  x2n[0] = GF_X;
+  for (int k = 1; k < 64; ++k) x2n[k] = gf_mul(x2n[k - 1], x2n[k - 1], poly);
+  const uint32_t X = xpow_tab(x2n, 8ull * K * STEP, poly);
+  t.p[0] = GF_ONE;
+  for (unsigned e = 1; e < CK_RIDE_MAX_GRID; ++e) t.p[e] = gf_mul(t.p[e - 1], X, poly);
+  return t;
+}
+static __constant__ const CkRidePow kRide32[3] = {make_ride_pow(POLY_CRC32, 4), make_ride_pow(POLY_CRC32, 8),
+                                                  make_ride_pow(POLY_CRC32, 16)};
+static __constant__ const CkRidePow kRide32c[3] = {make_ride_pow(POLY_CRC32C, 4), make_ride_pow(POLY_CRC32C, 8),
+                                                   make_ride_pow(POLY_CRC32C, 16)};
+template <int KIND, int K>
+MC_DEV const CkRidePow &ride_pow() {
+  constexpr int i = K == 4 ? 0 : K == 8 ? 1 : 2;
+  if constexpr (KIND == K_CRC32C) return kRide32c[i];
+  else return kRide32[i];
+}
+
 // ---------------------------------------------------------------------------
 // CRC tiles with the bit-sliced fold (crc_fold_bs, K >= 4): no LDS tables;
 // workgroups loop over tiles (grid: ck_grid_cap_bs) with the next tile's K
@@ -14,6 +41,11 @@ namespace mcck {
 // alignment x^(-128 l) uses the 32 products g * x^i kept in registers (one
 // v_bitop3 + one v_bfe per bit); the four wave partials of a tile go through
 // a parity-double-buffered LDS slot, one barrier per tile.
+// FUSED (one chunk, grid <= CK_RIDE_MAX_GRID): no partial stores.  The lane
+// alignment constant also carries the workgroup's shift to the chunk end
+// (g * X^e, e = (tiles - 1 - b) mod G), so its tile sums come out shifted;
+// wave 0 sums them by Horner with X^G on the scalar unit (the basis in the
+// kernel arguments) and arrives through ck_ride_arrive.
 // ---------------------------------------------------------------------------
 template <int KIND, int K, bool COPY, int ALS, int ALD, bool FUSED>
 __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
@@ -23,11 +55,10 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
   static_assert(KIND != K_ADLER && K >= 4, "bit-sliced folds exist for CRC tiles of 4, 8, 16 vectors");
   __shared__ uint32_t red[2][MC_BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t gx[32];  // g * x^i, g = x^(-128 threadIdx.x)
-  gx[0] = crc_consts<KIND>().g[threadIdx.x];
-#pragma unroll
-  for (int i = 1; i < 32; ++i) gx[i] = mulx_r<KIND>(gx[i - 1]);
+  uint32_t gx[32];  // g * x^i, g = x^(-128 threadIdx.x) (FUSED: times the workgroup's shift)
   constexpr size_t TB = (size_t)K * STEP;
+  constexpr uint32_t poly = crc_poly<KIND>();
+  uint32_t hz = 0;  // FUSED, wave 0: sum over this workgroup's tiles so far (wave-uniform)
   auto load = [&](mc_u32x4 (&v)[K], size_t tile) {
     const size_t c = tile / tiles_per_chunk, t = tile - c * tiles_per_chunk;
     ck_load_tile<K, ALS>(v, src + c * src_stride, t * TB + 16 * (size_t)threadIdx.x, n, (t + 1) * TB <= n);
@@ -56,17 +87,44 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
     p = wave_xor(p);
     if (lane == 0) red[par][wave] = p;
     __syncthreads();  // red[par] is rewritten two tiles later, after the next barrier
-    if (threadIdx.x == 0) {
+    if constexpr (FUSED) {
+      if (__builtin_amdgcn_readfirstlane(wave) == 0) {  // (wave-uniform: the sum stays scalar)
+        uint32_t r = 0;
+#pragma unroll
+        for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= red[par][w];
+        uint32_t m = 0;  // hz * X^G
+#pragma unroll
+        for (int i = 0; i < 32; ++i) m ^= ((hz >> i) & 1u) ? fin.xgb[i] : 0u;
+        hz = m ^ __builtin_amdgcn_readfirstlane(r);
+      }
+    } else if (threadIdx.x == 0) {
       uint32_t r = 0;
 #pragma unroll
       for (int w = 0; w < MC_BLOCK / 64; ++w) r ^= red[par][w];
-      if constexpr (FUSED) __hip_atomic_store(&partials[tile], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else partials[tile] = r;
+      partials[tile] = r;
     }
   };
   mc_u32x4 a[K], b[K];
   size_t tile = blockIdx.x;
   if (tile < total_tiles) load(a, tile);
+  // while the first tile loads: the lane constants, and for the finish the
+  // stored word, each byte in a register of its own and nothing computed
+  // from them until the finish -- a use here waits for every load issued
+  // before (the tile's too: vmcnt counts in order), and the next tile's loads
+  // would issue only after the first tile arrived (tools/probe_ck_tail.py:
+  // a tail folded this way instead of a ragged last tile took 47 -> 58 us)
+  uint32_t g = crc_consts<KIND>().g[threadIdx.x];
+  uint32_t hb[4] = {0, 0, 0, 0};
+  if constexpr (FUSED) {
+    g = gf_mul(ride_pow<KIND, K>().p[(total_tiles - 1 - blockIdx.x) % gridDim.x], g, poly);
+    if (threadIdx.x == 0 && fx.stored) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hb[j] = fx.stored[j];
+    }
+  }
+  gx[0] = g;
+#pragma unroll
+  for (int i = 1; i < 32; ++i) gx[i] = mulx_r<KIND>(gx[i - 1]);
   while (tile < total_tiles) {
     const size_t t1 = tile + gridDim.x;
     if (t1 < total_tiles) load(b, t1);
@@ -77,7 +135,8 @@ __global__ __launch_bounds__(MC_BLOCK, 2) void k_crc_tiles_bs(
     fold(b, t1, 1);
     tile = t2;
   }
-  if constexpr (FUSED) ck_fused_tail<KIND, K>(fin, partials, tiles_per_chunk, n, src_stride, fx);
+  if constexpr (FUSED)
+    if (threadIdx.x == 0 && ck_ride_arrive(fx.ticket, hz)) ck_ride_finish<KIND>(fin, fx, hz, hb);
 }
 
 namespace {

@@ -448,3 +448,72 @@ def test_one_launch_encode_abi(device, kind_name):
     torch.cuda.synchronize()
     assert not ticket.any()
     assert _ops._CK_FUSED_ENCODE_MAX < (17 << 20)  # both schedules ran through the codecs above
+
+
+@pytest.mark.parametrize("codec_id", ["crc32", "crc32c"])
+def test_one_launch_crc_arrival_tree(device, codec_id):
+    """The bit-sliced CRC kernel's one-launch finish (ck_ride_arrive): the
+    workgroups' shifted sums ride a 32-ary tree of returning XOR atomics.
+    Tile counts (64 KiB tiles for the verify) around the tree's shapes --
+    one level (<= 32 workgroups), two (33..1024), three (1025..2048) and
+    grids of 2048 whose workgroups fold 2 or 3 tiles (2049, 4097: the
+    stored word alone past the tiles) -- at both locations with several
+    init values; last tiles of 1..17 bytes; then the
+    copy-fused encode (32 KiB tiles, 1024
+    workgroups); the stream's arrival ticket is left zero."""
+    from numcodecs_amd import _native, _ops
+    from numcodecs_amd._native import lib
+
+    kind = {"crc32": _native.MC_CK_CRC32, "crc32c": _native.MC_CK_CRC32C}[codec_id]
+    T = 1 << 16
+    for tiles in (2, 31, 32, 33, 64, 65, 1056, 1057, 2048, 2049, 4097):
+        for loc_name, loc in (("start", _native.MC_CK_START), ("end", _native.MC_CK_END)):
+            n = tiles * T - 4 - (tiles % 7) if tiles != 4097 else (1 << 28)
+            x = RNG.integers(0, 256, n, dtype=np.uint8)
+            for v in ((0, 0x9E3779B9) if tiles in (33, 2049, 4097) else (0,)):
+                want = REF[codec_id](x, v)
+                stored = np.array([want], dtype="<u4").view(np.uint8)
+                buf = torch.from_numpy(np.concatenate([stored, x] if loc_name == "start" else [x, stored])).to(device)
+                assert buf.data_ptr() % 16 == 0
+                got = _ops.checksum32_verify(kind, buf, n + 4, v, loc)
+                assert got == (want, want), (codec_id, tiles, loc_name, v)
+                if v == 0:
+                    bad = buf.clone()
+                    bad[(4 if loc_name == "start" else 0) + (n * 5) // 7] ^= 0x10
+                    got = _ops.checksum32_verify(kind, bad, n + 4, v, loc)
+                    assert got[0] != want and got[1] == want, (codec_id, tiles, loc_name)
+                del buf
+    # last tiles holding 1..17 bytes, a corrupted byte among them
+    for extra in (1, 4, 12, 16, 17):
+        for loc_name, loc in (("start", _native.MC_CK_START), ("end", _native.MC_CK_END)):
+            n = 40 * T + extra - (4 if loc_name == "start" else 0)
+            x = RNG.integers(0, 256, n, dtype=np.uint8)
+            for v in (0, 0x5A5A5A5A):
+                want = REF[codec_id](x, v)
+                stored = np.array([want], dtype="<u4").view(np.uint8)
+                buf = torch.from_numpy(np.concatenate([stored, x] if loc_name == "start" else [x, stored])).to(device)
+                assert _ops.checksum32_verify(kind, buf, n + 4, v, loc) == (want, want), (codec_id, extra, loc_name)
+                bad = buf.clone()
+                bad[-1 if loc_name == "start" else n - 1] ^= 0x80  # the payload's last byte: in the tail
+                got = _ops.checksum32_verify(kind, bad, n + 4, v, loc)
+                assert got[0] != want and got[1] == want, (codec_id, extra, loc_name, v)
+    st = torch.cuda.current_stream(device).cuda_stream
+    ticket = torch.zeros(_native.MC_ARRIVAL_WORDS, dtype=torch.int32, device=device)
+    for n in (2 * (1 << 15) - 5, 33 * (1 << 15) - 1, 1025 * (1 << 15) + 3, (64 << 20) + 5):
+        x = RNG.integers(0, 256, n, dtype=np.uint8)
+        xd = torch.from_numpy(x).to(device)
+        for loc_name, loc in (("start", _native.MC_CK_START), ("end", _native.MC_CK_END)):
+            ref = oracle.checksum32_encode(codec_id, x, location=loc_name)
+            dst = torch.full((n + 4,), 0xAB, dtype=torch.uint8, device=device)
+            out = torch.zeros(1, dtype=torch.int32, device=device)
+            ws = torch.empty(max(lib.mc_checksum32_workspace(kind, 1, n), 16), dtype=torch.uint8, device=device)
+            _native.check(lib.mc_checksum32_encode_fused(kind, xd.data_ptr(), dst.data_ptr(), n, 0, None, 0, loc,
+                                                         out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                         ticket.data_ptr(), st))
+            assert np.array_equal(dst.cpu().numpy(), ref), (n, loc_name)
+            assert int(out.cpu().numpy().view(np.uint32)[0]) == REF[codec_id](x), (n, loc_name)
+    torch.cuda.synchronize()
+    assert not ticket.any()
+    for (dev_idx, _), sl in _ops._TLS.slots.items():
+        if dev_idx == device.index:
+            assert not sl.ticket.any()
