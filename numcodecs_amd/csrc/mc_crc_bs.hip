@@ -184,6 +184,9 @@ int launch_kind(int K, int als, int ald, const uint8_t *s, size_t ss, uint8_t *d
 int launch_crc_bs(int kind, int K, int als, int ald, const uint8_t *s, size_t ss, uint8_t *d, size_t ds,
                   size_t n, size_t tpc, size_t total, uint32_t *parts, const CrcFin &fin, const CkFinish *fx,
                   unsigned grid, hipStream_t st) {
+  // the one-launch encode's payload copy to an aligned destination: the
+  // dword-aligned (plain) 16-B store variant when ck_fused_plain is set
+  if (fx && d && ald == 2 && mc_sched.ck_fused_plain) ald = 1;
   if (kind == MC_CK_CRC32)
     return launch_kind<K_CRC32>(K, als, ald, s, ss, d, ds, n, tpc, total, parts, fin, fx, grid, st);
   if (kind == MC_CK_CRC32C)

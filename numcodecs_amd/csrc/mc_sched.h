@@ -30,6 +30,7 @@ struct mc_sched_t {
   int crc_lds;         // CRC32/CRC32C tiles of >= 4 vectors per lane fold with the LDS slicing-by-16 tables (1) or bit-sliced XORs (0)
   int delta_enc_dv;    // same-type Delta encode (k_delta_enc_same): 16-B vectors per thread (4 or 8)
   int br_planes;       // BitRound+Shuffle(4) of one large chunk masks the planes (k_bitround_shuffle4_planes) (0/1)
+  int ck_fused_plain;  // one-launch CRC encode to a 16-B aligned destination: plain (1) or nontemporal (0) 16-B stores
 };
 
 extern mc_sched_t mc_sched __attribute__((visibility("hidden")));

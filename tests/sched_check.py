@@ -189,6 +189,7 @@ PLAN = {
     "crc_lds": ([1], check_checksums),
     "delta_enc_dv": ([8], check_delta_same_type),
     "br_planes": ([0], check_bitround_shuffle),
+    "ck_fused_plain": ([1], check_checksums),
 }
 
 

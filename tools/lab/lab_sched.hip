@@ -40,6 +40,7 @@ const field kFields[] = {
     {"crc_lds", "MCODEC_CRC_LDS", &mc_sched.crc_lds},
     {"delta_enc_dv", "MCODEC_DELTA_ENC_DV", &mc_sched.delta_enc_dv},
     {"br_planes", "MCODEC_BR_PLANES", &mc_sched.br_planes},
+    {"ck_fused_plain", "MCODEC_CK_FUSED_PLAIN", &mc_sched.ck_fused_plain},
 };
 
 __attribute__((constructor)) void lab_sched_from_env() {
