@@ -610,25 +610,24 @@ def checksum32(kind, src, src_stride, nchunks, nbytes, init, prefix=None) -> tor
 
 
 # Single-chunk Checksum32 encodes finish in the tiles launch (one launch: 1 MiB
-# CRC32 / Adler32 encode 14.2 / 14.5 -> 10.5 / 8.3 us per call).  CRC32 /
-# CRC32C at every size since round 6 (the workgroups' sums ride the arrival
-# atomics, ck_ride_arrive: 256 MiB 85.8 / 87.7 us against 93.9 / 90.6 for
-# tiles + finalize, tools/probe_ck_stamp.py); Adler32 below this size only
-# (at 256 MiB its separate finalize kernel measured ~3 us faster: every
-# block of the fused copy drains its payload stores before it arrives).
-_CK_FUSED_ENCODE_MAX = 16 << 20
+# CRC32 / Adler32 encode 14.2 / 14.5 -> 10.5 / 8.3 us per call), at every size
+# since round 6: with the workgroups' sums riding the arrival atomics
+# (CRC: ck_ride_arrive; Adler32: adler_arrive_finish) the one launch beats
+# tiles + finalize at 256 MiB by 5-6 us for all three checksums at both
+# footer locations (tools/probe_adler_encode.py, 4 rotating sets,
+# profiles/r06/probe_ck_encode_sets.jsonl); round 5 had measured Adler32's
+# finalize kernel ~3 us faster there and kept chunks >= 16 MiB on it.
 
 
 def checksum32_encode(kind, src, src_stride, dst, dst_stride, nchunks, nbytes, init, location,
                       prefix=None) -> None:
     """Checksum32.encode of `nchunks` rows into dst rows (LE32 footer at the start or end).
-    One chunk of CRC32 / CRC32C (Adler32 below _CK_FUSED_ENCODE_MAX) runs in
-    one launch (the stream's arrival ticket; the tiles-then-finalize schedule
-    during HIP-graph capture and for larger Adler32 chunks)."""
+    One chunk of CRC32 / CRC32C / Adler32 runs in one launch (the stream's
+    arrival ticket; the tiles-then-finalize schedule during HIP-graph
+    capture)."""
     _native.require_device()
     with _guard(src):
-        if nchunks == 1 and kind != _native.MC_CK_JENKINS and (kind != _native.MC_CK_ADLER32
-                                                               or nbytes < _CK_FUSED_ENCODE_MAX):
+        if nchunks == 1 and kind != _native.MC_CK_JENKINS:
             st = stream(src)
             sl = _verify_slot(src, st)
             if sl is not None:
