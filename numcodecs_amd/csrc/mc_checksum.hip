@@ -373,9 +373,15 @@ inline unsigned ck_grid_cap_bs(bool copy) {
 }
 
 // the bit-sliced kernel's grid; its one-launch finish (ck_ride_arrive) takes
-// at most CK_RIDE_MAX_GRID workgroups
+// at most CK_RIDE_MAX_GRID workgroups.  The one-launch verify runs one round
+// of resident workgroups (two per CU, 512): with the sums riding the arrival
+// atomics the 256 MiB verify measured 48.6 / 48.7 us per single launch
+// against 50.3 / 49.6 at 2048 (768-1536 were slower still;
+// tools/probe_ck_verify_grid6.py, profiles/r06/probe_ck_verify_grid6.jsonl)
+constexpr unsigned CK_VERIFY_GRID = 512;
 inline unsigned ck_bs_grid(size_t total, bool copy, bool fused) {
   unsigned cap = ck_grid_cap_bs(copy);
+  if (fused && !copy && mc_sched.ck_grid <= 0) cap = CK_VERIFY_GRID;
   if (fused && cap > CK_RIDE_MAX_GRID) cap = CK_RIDE_MAX_GRID;
   return (unsigned)(total < cap ? total : cap);
 }
