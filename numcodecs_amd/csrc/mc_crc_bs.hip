@@ -33,7 +33,7 @@ MC_DEV const CkRidePow &ride_pow() {
 
 // ---------------------------------------------------------------------------
 // CRC tiles with the bit-sliced fold (crc_fold_bs, K >= 4): no LDS tables;
-// workgroups loop over tiles (grid: ck_grid_cap_bs) with the next tile's K
+// workgroups loop over tiles (grid: ck_bs_grid) with the next tile's K
 // vectors loaded into a second register set before the current tile is
 // folded (the fold is ~3 VALU ops per byte, so with one tile per workgroup
 // the loads and the XOR network of a workgroup serialise and ~half the wave
