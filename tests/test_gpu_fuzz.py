@@ -12,7 +12,7 @@ import warnings
 import numpy as np
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, example, given, settings
 from hypothesis import strategies as st
 
 import oracle
@@ -159,6 +159,41 @@ def test_fuzz_checksum32(device, n, seed, off, cid, loc):
     codec = {"crc32": CRC32, "crc32c": CRC32C, "adler32": Adler32}[cid](location=loc)
     enc = codec.encode(_dev(x, device)[off:])
     assert enc.cpu().numpy().tobytes() == oracle.checksum32_encode(cid, x[off:], loc).tobytes()
+    assert np.array_equal(codec.decode(enc).cpu().numpy(), x[off:])
+
+
+FUZZ_BIG = settings(max_examples=40, deadline=None, derandomize=True, database=None,
+                    suppress_health_check=list(HealthCheck))
+
+
+@FUZZ_BIG
+@given(tiles=st.integers(1, 2100), rem=st.integers(-8, 8), seed=st.integers(0, 2**32 - 1),
+       off=st.sampled_from([0, 0, 4, 8, 1]), cid=st.sampled_from(["crc32", "crc32c", "adler32"]),
+       loc=st.sampled_from(["start", "end"]), flip=st.integers(0, 2**40))
+@example(tiles=2049, rem=4, seed=1, off=0, cid="crc32", loc="start", flip=123456789)
+@example(tiles=1025, rem=-3, seed=2, off=1, cid="crc32c", loc="end", flip=987654321)
+@example(tiles=513, rem=0, seed=3, off=4, cid="adler32", loc="start", flip=5)
+@example(tiles=2100, rem=8, seed=4, off=8, cid="crc32c", loc="start", flip=2**39)
+def test_fuzz_checksum32_one_launch(device, tiles, rem, seed, off, cid, loc, flip):
+    """The one-launch encode and verify (the workgroups' sums riding the
+    arrival atomics) over chunks of up to ~2100 tiles of 64 KiB with ragged
+    ends, aligned and misaligned, at both locations; a flipped payload bit
+    must fail the verify with the reference's error."""
+    n = max(1, tiles * 65536 + rem)
+    x = _raw(seed, n + off)
+    codec = {"crc32": CRC32, "crc32c": CRC32C, "adler32": Adler32}[cid](location=loc)
+    xd = _dev(x, device)[off:]
+    enc = codec.encode(xd)
+    ref = oracle.checksum32_encode(cid, x[off:], loc)
+    assert enc.cpu().numpy().tobytes() == ref.tobytes()
+    assert torch.equal(codec.decode(enc), xd)
+    big = torch.empty(enc.numel() + 16, dtype=torch.uint8, device=device)
+    view = big[off: off + enc.numel()]
+    view.copy_(enc)
+    k = (4 if loc == "start" else 0) + flip % n
+    view[k] ^= 1 << (flip % 8)
+    with pytest.raises(RuntimeError, match="checksum do not match"):
+        codec.decode(view)
 
 
 @FUZZ
