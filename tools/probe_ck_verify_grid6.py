@@ -5,7 +5,7 @@ ck_grid): back-to-back launches (10 between one event pair) and single
 launches (event pair around each, stream idle before), interleaved rounds.
 One JSON line per (kind, grid).
 
-Usage: python tools/probe_ck_verify_grid6.py"""
+Usage: python tools/probe_ck_verify_grid6.py   (CK_ADLER=1: Adler32 instead)"""
 import ctypes
 import json
 import os
@@ -67,11 +67,16 @@ def single(fn, reps=10):
     return ts[len(ts) // 2]
 
 
+KINDS = ((_native.MC_CK_CRC32, "CRC32"), (_native.MC_CK_CRC32C, "CRC32C"))
+GRIDS = (512, 768, 1024, 1536, 2048)
+if os.environ.get("CK_ADLER") == "1":  # Adler32's one-launch verify over its grid cap
+    KINDS = ((_native.MC_CK_ADLER32, "Adler32"),)
+    GRIDS = (512, 1024, 2048, 4096)
 res = {}
 ref = {}
 for rnd in range(4):
-    for kind, name in ((_native.MC_CK_CRC32, "CRC32"), (_native.MC_CK_CRC32C, "CRC32C")):
-        for g in (512, 768, 1024, 1536, 2048):
+    for kind, name in KINDS:
+        for g in GRIDS:
             lab.mc_lab_set_sched(b"ck_grid", g)
             ver(kind, 0)
             torch.cuda.synchronize()
