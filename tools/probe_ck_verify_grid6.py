@@ -5,7 +5,8 @@ ck_grid): back-to-back launches (10 between one event pair) and single
 launches (event pair around each, stream idle before), interleaved rounds.
 One JSON line per (kind, grid).
 
-Usage: python tools/probe_ck_verify_grid6.py   (CK_ADLER=1: Adler32 instead)"""
+Usage: python tools/probe_ck_verify_grid6.py   (CK_ADLER=1: Adler32 instead;
+CK_KSWEEP=1: CRC32C with 32 and 64 KiB tiles)"""
 import ctypes
 import json
 import os
@@ -69,24 +70,31 @@ def single(fn, reps=10):
 
 KINDS = ((_native.MC_CK_CRC32, "CRC32"), (_native.MC_CK_CRC32C, "CRC32C"))
 GRIDS = (512, 768, 1024, 1536, 2048)
+KS = (0,)  # ck_k: 0 = the product's tile size
 if os.environ.get("CK_ADLER") == "1":  # Adler32's one-launch verify over its grid cap
     KINDS = ((_native.MC_CK_ADLER32, "Adler32"),)
     GRIDS = (512, 1024, 2048, 4096)
+if os.environ.get("CK_KSWEEP") == "1":  # 32 KiB tiles (fewer registers: three waves per SIMD) too
+    KINDS = ((_native.MC_CK_CRC32C, "CRC32C"),)
+    GRIDS = (512, 768, 1024)
+    KS = (8, 16)
 res = {}
 ref = {}
 for rnd in range(4):
     for kind, name in KINDS:
-        for g in GRIDS:
+        for g, kk in [(g, kk) for g in GRIDS for kk in KS]:
             lab.mc_lab_set_sched(b"ck_grid", g)
+            lab.mc_lab_set_sched(b"ck_k", kk)
             ver(kind, 0)
             torch.cuda.synchronize()
             got = tuple(int(v) for v in rec[:2].cpu())
             assert ref.setdefault(name, got) == got, (name, g)
-            res.setdefault((name, g, "b2b"), []).append(b2b(lambda i: ver(kind, i)))
-            res.setdefault((name, g, "single"), []).append(single(lambda i: ver(kind, i)))
+            res.setdefault((name, g, kk, "b2b"), []).append(b2b(lambda i: ver(kind, i)))
+            res.setdefault((name, g, kk, "single"), []).append(single(lambda i: ver(kind, i)))
 lab.mc_lab_set_sched(b"ck_grid", 0)
-for (name, g, mode), ts in res.items():
+lab.mc_lab_set_sched(b"ck_k", 16)
+for (name, g, kk, mode), ts in res.items():
     ts.sort()
-    print(json.dumps({"probe": "ck_verify_grid6", "kind": name, "ck_grid": g, "mode": mode,
+    print(json.dumps({"probe": "ck_verify_grid6", "kind": name, "ck_grid": g, "ck_k": kk or 16, "mode": mode,
                       "us_med": round(ts[len(ts) // 2], 2), "us_min": round(ts[0], 2)}), flush=True)
 assert not ticket.any()
