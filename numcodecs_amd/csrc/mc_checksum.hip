@@ -345,6 +345,16 @@ inline int ck_kbig() {
   const int e = mc_sched.ck_k;
   return (e == 4 || e == 8 || e == 16) ? e : 16;
 }
+// the one-launch CRC verify's tile: 32 KiB (K = 8: 159 VGPRs, three waves per
+// SIMD) on one round of 768 workgroups, against 64 KiB tiles on 512: 256 MiB
+// CRC32 / CRC32C 46.0 / 45.6 us back to back (47.8 / 47.4 single) against
+// 47.8 / 46.6 (48.9 / 48.0); 16 KiB tiles 52-66 us
+// (tools/probe_ck_verify_grid6.py CK_KSWEEP=1, profiles/r06/probe_crc_verify_k.jsonl)
+constexpr int CK_VERIFY_K = 8;
+inline int ck_k_verify(size_t n) {
+  const int e = mc_sched.ck_k;
+  return n < (size_t)16 * STEP ? 1 : (e == 4 || e == 8 || e == 16) ? e : CK_VERIFY_K;
+}
 inline int ck_kcopy() {
   const int e = mc_sched.ck_kcopy;
   return (e == 4 || e == 8 || e == 16) ? e : 8;
@@ -374,11 +384,12 @@ inline unsigned ck_grid_cap_bs(bool copy) {
 
 // the bit-sliced kernel's grid; its one-launch finish (ck_ride_arrive) takes
 // at most CK_RIDE_MAX_GRID workgroups.  The one-launch verify runs one round
-// of resident workgroups (two per CU, 512): with the sums riding the arrival
-// atomics the 256 MiB verify measured 48.6 / 48.7 us per single launch
-// against 50.3 / 49.6 at 2048 (768-1536 were slower still;
-// tools/probe_ck_verify_grid6.py, profiles/r06/probe_ck_verify_grid6.jsonl)
-constexpr unsigned CK_VERIFY_GRID = 512;
+// of resident workgroups (three per CU with CK_VERIFY_K's registers, 768):
+// with the sums riding the arrival atomics, one round beat four (64 KiB
+// tiles: 48.6 / 48.7 us per single launch on 512 workgroups against 50.3 /
+// 49.6 on 2048; tools/probe_ck_verify_grid6.py,
+// profiles/r06/probe_ck_verify_grid6.jsonl)
+constexpr unsigned CK_VERIFY_GRID = 768;
 inline unsigned ck_bs_grid(size_t total, bool copy, bool fused) {
   unsigned cap = ck_grid_cap_bs(copy);
   if (fused && !copy && mc_sched.ck_grid <= 0) cap = CK_VERIFY_GRID;
@@ -390,10 +401,11 @@ inline unsigned ck_bs_grid(size_t total, bool copy, bool fused) {
 inline int ck_k(size_t n, bool copy) {
   return n < (size_t)16 * STEP ? 1 : copy ? ck_kcopy() : ck_kbig();
 }
-// the workspace covers either pass
+// the workspace covers every pass
 inline int ck_k_ws(size_t n) {
-  const int a = ck_k(n, false), b = ck_k(n, true);
-  return a < b ? a : b;
+  const int a = ck_k(n, false), b = ck_k(n, true), c = ck_k_verify(n);
+  const int m = a < b ? a : b;
+  return m < c ? m : c;
 }
 inline size_t ck_tiles(size_t n, int K) {
   const size_t tb = (size_t)K * STEP;
@@ -531,13 +543,13 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   // n payload bytes; the tiles cover all n + 4 (one-launch verify only)
   const size_t np = n;
   n += head;
-  const int K = ck_k(n, d != nullptr);
+  // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
+  const bool fused = ticket && nchunks == 1;
+  const int K = fused && !d && KIND != K_ADLER && !mc_sched.crc_lds ? ck_k_verify(n) : ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;
   uint32_t *parts = static_cast<uint32_t *>(ws);
-  // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
-  const bool fused = ticket && nchunks == 1;
   CkFinish fx{init, seq, head, ticket, out, stored_out, footer, fs, stored, 0};
   const unsigned G = ck_bs_grid(tpc * nchunks, d != nullptr, fused);
   switch (K) {

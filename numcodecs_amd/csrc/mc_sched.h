@@ -13,7 +13,7 @@
 struct mc_sched_t {
   int copy_u;          // mc_copy: 16-B vectors per thread per tile (4 or 8)
   int copy_grid;       // mc_copy: workgroup cap, 0 = one tile per workgroup
-  int ck_k;            // checksum-only passes: tile = ck_k x 4 KiB (4, 8, 16)
+  int ck_k;            // checksum-only passes: tile = ck_k x 4 KiB (4, 8, 16; 0 = per-pass default)
   int ck_kcopy;        // copying checksum passes: tile = ck_kcopy x 4 KiB (4, 8, 16)
   int ck_grid;         // checksum-only grid cap, 0 = per-kind default
   int ck_grid_copy;    // copying checksum passes' grid cap

@@ -172,7 +172,7 @@ def check_bitround_shuffle():
 PLAN = {
     "copy_u": ([8], check_copy),
     "copy_grid": ([64, 2048], check_copy),
-    "ck_k": ([4, 8], check_checksums),
+    "ck_k": ([4, 8, 16], check_checksums),
     "ck_kcopy": ([4, 16], check_checksums),
     "ck_grid": ([256, 1024], check_checksums),
     "ck_grid_copy": ([128, 4096], check_checksums),
