@@ -6,7 +6,7 @@ either way), "end" at the 16-B aligned dst.  Interleaved rounds, outputs
 compared with the product library's.  One JSON line per case.
 
 Usage: python tools/probe_ck_encode.py   (CK_SWEEP=1: the copying pass's tile
-size x grid instead)"""
+size x grid instead; CK_SWEEP_K4=1: 16 / 32 KiB tiles x 768-1536 workgroups)"""
 import ctypes
 import json
 import os
@@ -56,13 +56,16 @@ def timed(fn, reps=10):
 
 
 SWEEP = os.environ.get("CK_SWEEP") == "1"
+KCS, GRIDS = (8, 16), (512, 1024, 2048)
+if os.environ.get("CK_SWEEP_K4") == "1":  # 16 KiB tiles (four waves per SIMD) against 32 KiB
+    SWEEP, KCS, GRIDS = True, (4, 8), (768, 1024, 1536)
 if SWEEP:  # tile size and grid of the copying pass, nontemporal stores
     res = {}
     for rnd in range(3):
         for kind, name in ((_native.MC_CK_CRC32, "CRC32"), (_native.MC_CK_CRC32C, "CRC32C")):
             for loc_name, loc in (("start", _native.MC_CK_START), ("end", _native.MC_CK_END)):
-                for kc in (8, 16):
-                    for g in (512, 1024, 2048):
+                for kc in KCS:
+                    for g in GRIDS:
                         lab.mc_lab_set_sched(b"ck_kcopy", kc)
                         lab.mc_lab_set_sched(b"ck_grid_copy", g)
                         t = timed(lambda i: enc(lab, kind, loc, i))
