@@ -6,7 +6,7 @@ launches (event pair around each, stream idle before), interleaved rounds.
 One JSON line per (kind, grid).
 
 Usage: python tools/probe_ck_verify_grid6.py   (CK_ADLER=1: Adler32 instead;
-CK_KSWEEP=1: CRC32C with 32 and 64 KiB tiles)"""
+CK_KSWEEP=1: 16, 32 and 64 KiB tiles)"""
 import ctypes
 import json
 import os
@@ -74,10 +74,9 @@ KS = (0,)  # ck_k: 0 = the product's tile size
 if os.environ.get("CK_ADLER") == "1":  # Adler32's one-launch verify over its grid cap
     KINDS = ((_native.MC_CK_ADLER32, "Adler32"),)
     GRIDS = (512, 1024, 2048, 4096)
-if os.environ.get("CK_KSWEEP") == "1":  # 32 KiB tiles (fewer registers: three waves per SIMD) too
-    KINDS = ((_native.MC_CK_CRC32C, "CRC32C"),)
+if os.environ.get("CK_KSWEEP") == "1":  # 16 / 32 KiB tiles too (fewer registers: 4 / 3 waves per SIMD)
     GRIDS = (512, 768, 1024)
-    KS = (8, 16)
+    KS = (4, 8, 16)
 res = {}
 ref = {}
 for rnd in range(4):

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: CRC32C verify, 32 vs 64 KiB tiles over the grid (lab)
+# round 6: CRC verify, 16 / 32 / 64 KiB tiles over the grid (lab)
 set -u
 cd "${GRAFT_REPO_ROOT}"; mkdir -p gpurun_out/r6u
 export TMPDIR=/tmp
