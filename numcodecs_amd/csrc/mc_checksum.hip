@@ -345,12 +345,15 @@ inline int ck_kbig() {
   const int e = mc_sched.ck_k;
   return (e == 4 || e == 8 || e == 16) ? e : 16;
 }
-// the one-launch CRC verify's tile: 32 KiB (K = 8: 159 VGPRs, three waves per
-// SIMD) on one round of 768 workgroups, against 64 KiB tiles on 512: 256 MiB
-// CRC32 / CRC32C 46.0 / 45.6 us back to back (47.8 / 47.4 single) against
-// 47.8 / 46.6 (48.9 / 48.0); 16 KiB tiles 52-66 us
-// (tools/probe_ck_verify_grid6.py CK_KSWEEP=1, profiles/r06/probe_crc_verify_k.jsonl)
+// the one-launch verify's tile: 32 KiB.  CRC (K = 8: 159 VGPRs, three waves
+// per SIMD) on one round of 768 workgroups, against 64 KiB tiles on 512: 256
+// MiB CRC32 / CRC32C 46.0 / 45.6 us back to back (47.8 / 47.4 single) against
+// 47.8 / 46.6 (48.9 / 48.0); 16 KiB tiles 52-66 us (tools/probe_ck_verify_grid6.py
+// CK_KSWEEP=1, profiles/r06/probe_crc_verify_k.jsonl).  Adler32 on 1024
+// workgroups: 44.6 us back to back (46.9 single) against 47.3 (51.8) for 64
+// KiB tiles on 2048 (CK_ADLER=1 CK_KSWEEP=1, probe_adler_verify_k.jsonl)
 constexpr int CK_VERIFY_K = 8;
+constexpr unsigned ADLER_VERIFY_GRID = 1024;
 inline int ck_k_verify(size_t n) {
   const int e = mc_sched.ck_k;
   return n < (size_t)16 * STEP ? 1 : (e == 4 || e == 8 || e == 16) ? e : CK_VERIFY_K;
@@ -419,7 +422,8 @@ inline int align_class(const void *p, size_t stride, size_t nchunks) {
 template <int KIND, int K, bool COPY, int ALS, int ALD>
 void launch_tiles(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t n, size_t tpc,
                   size_t total, uint32_t *parts, const CrcFin &fin, const CkFinish *fx, hipStream_t st) {
-  const unsigned cap = ck_grid_cap(COPY, KIND != K_ADLER);
+  unsigned cap = ck_grid_cap(COPY, KIND != K_ADLER);
+  if (fx && KIND == K_ADLER && !COPY && mc_sched.ck_grid <= 0) cap = ADLER_VERIFY_GRID;  // (CK_VERIFY_K)
   const unsigned grid = (unsigned)(total < cap ? total : cap);
   if (fx) {  // one chunk: the last block finishes it in this launch (verify, or encode with its copy)
     const unsigned fg = KIND == K_ADLER && grid > ADLER_MAX_GRID ? ADLER_MAX_GRID : grid;
@@ -545,7 +549,7 @@ int run_reduction(const uint8_t *s, size_t ss, uint8_t *d, size_t ds, size_t nch
   n += head;
   // one chunk with a ticket: finish in the tiles launch (ck_finish_chunk)
   const bool fused = ticket && nchunks == 1;
-  const int K = fused && !d && KIND != K_ADLER && !mc_sched.crc_lds ? ck_k_verify(n) : ck_k(n, d != nullptr);
+  const int K = fused && !d && (KIND == K_ADLER || !mc_sched.crc_lds) ? ck_k_verify(n) : ck_k(n, d != nullptr);
   const size_t tpc = ck_tiles(n, K);
   const size_t need = tpc * nchunks * (KIND == K_ADLER ? 8 : 4);
   if (!ws || ws_bytes < need) return MC_ENOSPC;

@@ -77,6 +77,8 @@ if os.environ.get("CK_ADLER") == "1":  # Adler32's one-launch verify over its gr
 if os.environ.get("CK_KSWEEP") == "1":  # 16 / 32 KiB tiles too (fewer registers: 4 / 3 waves per SIMD)
     GRIDS = (512, 768, 1024)
     KS = (4, 8, 16)
+    if os.environ.get("CK_ADLER") == "1":
+        GRIDS, KS = (1024, 2048, 4096), (8, 16)
 res = {}
 ref = {}
 for rnd in range(4):
