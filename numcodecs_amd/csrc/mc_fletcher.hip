@@ -488,9 +488,12 @@ static size_t fused_partials_bytes(unsigned nslices) {
 // (profiles/r01/fletcher32_knobs_ab.jsonl): 4 loads in flight and 32 KiB
 // slices take the one-pass decode from 116 to 100 us.
 // The one-launch single-chunk verify (no copy) defaults to 8 vectors in
-// flight and a 4096-block grid: 256 MiB verify kernel 44.1-44.3 us at
-// (2048, 4) -> 43.0 us at (4096, 8), interleaved A/B on MI355X; the copying
-// and batched passes keep 4 (profiles/r01/fletcher32_knobs_ab.jsonl).
+// flight (256 MiB verify kernel 44.1-44.3 us at (grid 2048, 4 vectors) ->
+// 43.0 us at (4096, 8), interleaved A/B on MI355X; the copying and batched
+// passes keep 4; profiles/r01/fletcher32_knobs_ab.jsonl) and, since round 6,
+// a 2048-block grid: with 8 vectors, 32 KiB slices, 43.7 / 46.4 us back to
+// back / single against 44.0 / 47.6 at 4096 (tools/probe_f32_verify_sched.py,
+// profiles/r06/probe_f32_verify_sched.jsonl).
 static int f32_unroll(bool fused_verify = false) {
   const int e = mc_sched.f32_unroll;
   if (e == 1 || e == 4 || e == 8) return e;
@@ -500,7 +503,7 @@ static bool f32_ntld() { return mc_sched.f32_ntld != 0; }
 // f32_fused_grid: block cap of the one-launch verify (256 .. 65536)
 static unsigned f32_fused_grid() {
   const int e = mc_sched.f32_fused_grid;
-  return (unsigned)(e >= 256 && e <= 65536 ? e : 4096);
+  return (unsigned)(e >= 256 && e <= 65536 ? e : 2048);
 }
 static size_t f32_slice_bytes() {
   const int e = mc_sched.f32_slice_kb;

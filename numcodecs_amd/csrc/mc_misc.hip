@@ -7,7 +7,7 @@
 mc_sched_t mc_sched = {
     /*copy_u*/ 4,         /*copy_grid*/ 0,     /*ck_k*/ 0,           /*ck_kcopy*/ 8,
     /*ck_grid*/ 0,        /*ck_grid_copy*/ 1024, /*f32_unroll*/ 0,    /*f32_ntld*/ 1,
-    /*f32_fused_grid*/ 4096, /*f32_slice_kb*/ 32, /*c4_group_mi*/ 128, /*delta_enc_vec*/ 1,
+    /*f32_fused_grid*/ 2048, /*f32_slice_kb*/ 32, /*c4_group_mi*/ 128, /*delta_enc_vec*/ 1,
     /*dscan*/ 1,          /*dscan_nt*/ 2,      /*fspec*/ 1,           /*fastdiv*/ 1,
     /*crc_lds*/ 0,        /*delta_enc_dv*/ 4,      /*br_planes*/ 1,       /*ck_fused_plain*/ 0,
 };
